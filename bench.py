@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X bilateral-filter family (BASELINE.json metric:
+"Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling").
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+
+One step = one filter application over each rank's row slab of a frame that is
+row-sharded across the N GPUs (one process per GPU, torch.distributed over
+RCCL/xGMI; N>1 is launched by torch.distributed.run). Before each step's kernel
+the ranks exchange their r-row halos (sendrecv with the row neighbours only).
+
+  c2 (default) bilateral r=7 (ksize 15, sigma_space 10, sigma_color 30); each rank
+     owns a full 3840x2160 RGB8 frame's worth of rows of an (N*2160)x3840 frame
+     -> weak scaling; at N=1 this is exactly BASELINE config 2.
+  c3 adaptive bilateral r=7, same geometry (BASELINE config 3).
+  c4 bilateral texture filter k=5, nitr=5 on 3840x2160 per rank, no halo
+     (independent frames; BASELINE config 4).
+  c5 bilateral r=15 (ksize 31) on ONE 16384x16384 frame row-tiled over the N
+     GPUs (strong scaling; BASELINE config 5).
+
+Inputs are synthetic (test/random_array-style uniform u8), resident in HBM before
+timing; 12 distinct input/output slabs rotate so the working set exceeds the
+256 MB Infinity Cache. Rank 0 prints ONE JSON line. The roofline object is for
+the dominant kernel, timed with HIP events on the stream it runs on; the CPU
+baseline (rank 0, N=1) is the oracle's include/cpp restatement on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (== f32 MFMA) peak
+NBUF = 12
+BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
+
+
+def circle_taps(r: int) -> int:
+    return sum(1 for ky in range(-r, r + 1) for kx in range(-r, r + 1) if kx * kx + ky * ky <= r * r)
+
+
+CONFIGS = {
+    "c2": dict(kind="bilateral", width=3840, rows_per_rank=2160, ksize=15, workload="bilateral r=7 3840x2160 RGB8"),
+    "c3": dict(kind="adaptive", width=3840, rows_per_rank=2160, ksize=15,
+               workload="adaptive bilateral r=7 3840x2160 RGB8"),
+    "c4": dict(kind="texture", width=3840, rows_per_rank=2160, ksize=5, nitr=5,
+               workload="bilateral texture k=5 nitr=5 3840x2160 RGB8"),
+    "c5": dict(kind="bilateral", width=16384, frame_height=16384, ksize=31,
+               workload="bilateral r=15 16384x16384 RGB8 row-tiled"),
+}
+# algorithmic FP32 operations per in-support tap: bilateral
+# ws*wc (1) + 3 fma (6) + sumk add (1) = 8; adaptive adds the offset distance
+# ((n-c)-o: 6, |.|+|.|+|.|: 2) = 16.
+FLOP_PER_TAP = {"bilateral": 8, "adaptive": 16}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg) -> dict:
+    """include/cpp numerics (oracle CPP profile, row-parallel threads) on a
+    bounded sample of the same workload. Test infrastructure, not the product."""
+    from oracle import oracle as o
+    threads = max(1, min(16, os.cpu_count() or 1))
+    w = cfg["width"]
+    k = cfg["ksize"]
+    if cfg["kind"] == "texture":
+        rows = 256
+        img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
+        t0 = time.perf_counter()
+        o.texture(img, k, cfg["nitr"], profile=o.CPP)
+        dt = time.perf_counter() - t0
+        return dict(value=rows * w / dt / 1e6, unit="Mpixels/s", cores=1, kind="port",
+                    sample=f"{w}x{rows} band, texture k={k} nitr={cfg['nitr']}, 1 thread (oracle CPP profile)")
+    rows = 2160 if k <= 15 else 256
+    img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
+    fn = o.adaptive if cfg["kind"] == "adaptive" else o.bilateral
+    fn(img[:64], k, profile=o.CPP, threads=threads)  # warm-up
+    t0 = time.perf_counter()
+    fn(img, k, profile=o.CPP, threads=threads)
+    dt = time.perf_counter() - t0
+    return dict(value=rows * w / dt / 1e6, unit="Mpixels/s", cores=threads, kind="port",
+                sample=f"{w}x{rows} frame, {cfg['kind']} ksize={k}, {threads} threads "
+                       f"(oracle CPP profile = include/cpp numerics, all k*k taps like the reference loop)")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    cfg = CONFIGS[args.config]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import various_image_processings_amd as vip
+    from various_image_processings_amd.filters import _TextureImpl
+    from various_image_processings_amd.sharded import ShardedBilateral, SlabGeometry
+
+    stream = torch.cuda.current_stream(dev)
+    w = cfg["width"]
+    k = cfg["ksize"]
+    r = k // 2
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(42 + rank)
+
+    if cfg["kind"] == "texture":
+        rows = cfg["rows_per_rank"]
+        frame_h = rows * world
+        geo = None
+        tex = _TextureImpl(w, rows, k, cfg["nitr"])
+        srcs = [torch.randint(0, 255, (rows, w, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(NBUF)]
+        dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
+
+        def step(i):
+            tex.execute(srcs[i % NBUF], dsts[i % NBUF], stream=stream)
+    else:
+        frame_h = cfg.get("frame_height", cfg.get("rows_per_rank", 0) * world)
+        sb = ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
+        geo = sb.geo
+        rows = geo.own
+        srcs = [torch.randint(0, 255, (geo.slab_rows, w, 3), dtype=torch.uint8, device=dev, generator=gen)
+                for _ in range(NBUF)]
+        dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
+        kstart = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        kend = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        timed = {"on": False, "i": 0}
+
+        def step(i):
+            from various_image_processings_amd.sharded import exchange_halo
+            if world > 1:
+                exchange_halo(srcs[i % NBUF], geo)
+            if timed["on"]:
+                kstart[timed["i"]].record(stream)
+            sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
+            if timed["on"]:
+                kend[timed["i"]].record(stream)
+                timed["i"] += 1
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    if cfg["kind"] != "texture":
+        timed["on"] = True
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(args.steps):
+        step(args.warmup + i)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if cfg["kind"] != "texture":
+        kernel_ms = sum(a.elapsed_time(b) for a, b in zip(kstart, kend)) / args.steps
+    else:
+        kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    px_per_rank = rows * w
+    total_px = px_per_rank * world if cfg["kind"] == "texture" or "rows_per_rank" in cfg else frame_h * w
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_px / (elapsed / args.steps) / 1e6
+
+    if cfg["kind"] == "texture":
+        # stage-wise algorithmic bytes per pixel per iteration: grad 3+4,
+        # blur_rtv 7+16, guide 16+3, JBF 6+3 = 58 B
+        bytes_launch = 58.0 * px_per_rank * cfg["nitr"]
+        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+        roof = dict(bound="hbm", achieved=round(achieved, 2), peak=PEAK_HBM_GBS, unit="GB/s",
+                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=None,
+                    kernel="whole texture pipeline per launch (gradient, blur_rtv, guide, JBF) x nitr",
+                    avg_launch_ms=round(kernel_ms, 4))
+    else:
+        taps = circle_taps(r)
+        flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
+        tflops = flops / (kernel_ms * 1e-3) / 1e12
+        hbm = 6.0 * px_per_rank / (kernel_ms * 1e-3) / 1e9
+        roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
+                    frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=None,
+                    kernel=f"{cfg['kind']}_kernel<R={r}>", avg_launch_ms=round(kernel_ms, 4),
+                    flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
+                    hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
+                             bytes_per_px=6))
+
+    out = {
+        "metric": BASELINE_METRIC if args.config == "c2" else f"Mpixels/sec {cfg['workload']}",
+        "value": round(value, 2),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if "frame_height" in cfg else "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic uniform u8 (torch.randint 0..254), resident in HBM",
+        "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
+                   "frame": f"{w}x{frame_h}", "rows_per_rank": rows,
+                   "parallelism": f"row-tiled x{world}" + (" + r-row halo sendrecv" if world > 1 and geo else "")},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(cfg)
+        except Exception as e:  # the baseline is reported, never required
+            out["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+/*
+ * vip.h — C ABI of the MI355X-native bilateral-filter family.
+ *
+ * Drop-in boundary for the reference's include/cuda/ headers' API
+ * (yuyuyu-bot/various_image_processings). Plain pointers and sizes only; every
+ * image pointer is a DEVICE pointer to dense interleaved 8-bit 3-channel data
+ * (or f32 where stated). `pitch` arguments are row strides in bytes; the
+ * reference API has no pitch, so its wrappers pass width*channels*sizeof(T).
+ * `stream` is a hipStream_t (NULL = the legacy default stream). Every run
+ * function is asynchronous on `stream`: the C++ wrappers in include/cuda/ add
+ * the device synchronisation the reference performs in its public methods.
+ *
+ * Return value: 0 on success, otherwise a hipError_t code, or one of the
+ * VIP_ERR_* codes below for argument errors (the reference printed launch errors
+ * to stderr and carried on, src/host_utilities.hpp:9-13).
+ */
+#ifndef VIP_H
+#define VIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VIP_ABI_VERSION 1
+
+/* numerics profile */
+#define VIP_NUMERICS_CUDA 0 /* as src/<filter>_impl.cu: float-coefficient LUTs, fused multiply-add accumulate */
+#define VIP_NUMERICS_CPP 1  /* as include/cpp/<filter>.hpp: double-coefficient LUTs, separate multiply and add */
+
+/* argument errors (hipError_t values stay below 1000) */
+#define VIP_ERR_INVALID_ARGUMENT 10001 /* null handle/pointer, non-positive size */
+#define VIP_ERR_UNSUPPORTED_KSIZE 10002 /* ksize even, < 3, or radius above the compiled set */
+#define VIP_ERR_ALIASING 10003 /* dst aliases src or guide (the kernels read neighbours other blocks write) */
+
+typedef struct vip_bilateral_s* vip_bilateral_t;
+typedef struct vip_adaptive_s* vip_adaptive_t;
+typedef struct vip_texture_s* vip_texture_t;
+
+int vip_abi_version(void);
+const char* vip_error_string(int code);
+/* Largest filter radius (ksize/2) the bilateral / adaptive kernels are compiled for. */
+int vip_max_radius(void);
+
+/* ---- device buffers: replaces DeviceImage<T> (include/cuda/device_image.hpp:4-16,
+ *      src/device_image.cu:5-52) ---- */
+int vip_malloc(void** d_ptr, size_t bytes);
+int vip_free(void* d_ptr);
+int vip_upload(void* d_dst, const void* h_src, size_t bytes);   /* blocking H2D */
+int vip_download(void* h_dst, const void* d_src, size_t bytes); /* blocking D2H */
+int vip_device_synchronize(void);
+int vip_stream_synchronize(void* stream);
+
+/* ---- bilateral / joint bilateral: CudaBilateralFilter
+ *      (include/cuda/bilateral_filter.hpp:9-24, src/bilateral_filter_impl.cu:204-310) ---- */
+int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space,
+                         float sigma_color, int numerics);
+int vip_bilateral_destroy(vip_bilateral_t h);
+/* Impl::bilateral_filter (:241-258) */
+int vip_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
+                      void* stream);
+/* Impl::joint_bilateral_filter (:260-280): colour weights from d_guide, sums of d_src */
+int vip_joint_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
+                            size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, void* stream);
+/* Row-band variant for row-sharded frames (no reference counterpart; multi-GPU C5).
+ * Filters `out_rows` rows of a handle-width image. Output row i is centred on source
+ * row i + src_row0; neighbour rows are clamped to [row_lo, row_hi) of d_src (row_lo
+ * may be negative-free halo bounds: rows below row_lo / above row_hi-1 replicate them,
+ * which is exactly the reference's replicate border at the frame edges). d_guide may
+ * be NULL (plain bilateral). */
+int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
+                           size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, int out_rows, int src_row0,
+                           int row_lo, int row_hi, void* stream);
+
+/* ---- adaptive bilateral: CudaAdaptiveBilateralFilter
+ *      (include/cuda/adaptive_bilateral_filter.hpp:9-19, src/adaptive_bilateral_filter_impl.cu:117-191) ---- */
+int vip_adaptive_create(vip_adaptive_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
+                        int numerics);
+int vip_adaptive_destroy(vip_adaptive_t h);
+int vip_adaptive_run(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
+                     void* stream);
+int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
+                          int out_rows, int src_row0, int row_lo, int row_hi, void* stream);
+
+/* ---- gradient magnitude: cuda_gradient<T> (include/cuda/gradient.hpp:4-23, src/gradient_impl.cu:90-112) ---- */
+int vip_gradient_u8(const uint8_t* d_src, float* d_dst, int width, int height, int src_ch, int numerics,
+                    void* stream);
+int vip_gradient_f32(const float* d_src, float* d_dst, int width, int height, int src_ch, int numerics,
+                     void* stream);
+
+/* ---- bilateral texture filter: CudaBilateralTextureFilter
+ *      (include/cuda/bilateral_texture_filter.hpp:7-17, src/bilateral_texture_filter_impl.cu:179-275) ---- */
+int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int nitr, int numerics);
+int vip_texture_destroy(vip_texture_t h);
+/* Impl::execute (:199-214); d_src and d_dst are dense width*3 */
+int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream);
+/* Impl::compute_blur_and_rtv (:216-237): image u8x3, magnitude f32 -> blurred f32x3, rtv f32 */
+int vip_texture_blur_rtv(vip_texture_t h, const uint8_t* d_image, const float* d_magnitude, float* d_blurred,
+                         float* d_rtv, void* stream);
+/* Impl::compute_guide (:239-256): blurred f32x3, rtv f32 -> guide u8x3 */
+int vip_texture_guide(vip_texture_t h, const float* d_blurred, const float* d_rtv, uint8_t* d_guide, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VIP_H */

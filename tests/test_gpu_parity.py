@@ -1,0 +1,225 @@
+"""GPU parity tests: the HIP kernels (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact. The oracle's CUDA profile restates src/<filter>_impl.cu (float LUT
+coefficients, fused multiply-add), its CPP profile include/cpp (double LUT
+coefficients, multiply then add); the library implements both (numerics flag),
+so every u8 output must match exactly, and f32 stage outputs bit for bit.
+The reference's own tolerance (+-1 per channel, test/bilateral_filter.cu:58-60)
+is asserted separately between profiles.
+"""
+import numpy as np
+import pytest
+
+import various_image_processings_amd as vip
+from various_image_processings_amd.filters import _AdaptiveImpl, _BilateralImpl, _TextureImpl
+
+pytestmark = pytest.mark.gpu
+
+PROFILES = [(vip.VIP_NUMERICS_CUDA, 0), (vip.VIP_NUMERICS_CPP, 1)]
+
+
+def _bilateral_gpu(dev, img, k, ss=10.0, sc=30.0, numerics=0, guide=None):
+    h, w, _ = img.shape
+    f = vip.CudaBilateralFilter(w, h, k, ss, sc, numerics=numerics)
+    d_src, d_dst = dev.put(img), dev.empty((h, w, 3))
+    if guide is None:
+        f.bilateral_filter(d_src, d_dst)
+    else:
+        f.joint_bilateral_filter(d_src, dev.put(guide), d_dst)
+    return dev.get(d_dst)
+
+
+def _mismatch(a, b):
+    d = np.argwhere(a != b)
+    return f"{len(d)} mismatches, first {d[:5].tolist()} got {a[tuple(d[0])] if len(d) else None} " \
+           f"want {b[tuple(d[0])] if len(d) else None}"
+
+
+@pytest.mark.parametrize("k", [3, 5, 9, 11, 15, 21, 31])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_bilateral_reference_inputs(dev, oracle, k, numerics, profile):
+    img = oracle.random_image(50, 50)
+    got = _bilateral_gpu(dev, img, k, numerics=numerics)
+    want = oracle.bilateral(img, k, profile=profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (2, 3), (5, 7), (33, 130), (70, 129), (64, 257), (17, 4), (129, 1)])
+@pytest.mark.parametrize("k", [3, 15])
+def test_bilateral_ragged_shapes(dev, oracle, shape, k):
+    h, w = shape
+    img = oracle.random_u8(h * w * 3).reshape(h, w, 3)
+    got = _bilateral_gpu(dev, img, k)
+    want = oracle.bilateral(img, k)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("k,ss,sc", [(9, 10.0, 30.0), (15, 10.0, 30.0), (9, 4.0, 1.73205080757), (31, 20.0, 60.0)])
+def test_bilateral_large_frame(dev, oracle, k, ss, sc):
+    img = oracle.random_image(640, 360)
+    got = _bilateral_gpu(dev, img, k, ss, sc)
+    want = oracle.bilateral(img, k, ss, sc, threads=16)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("k", [3, 9, 15])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_joint_bilateral(dev, oracle, k, numerics, profile):
+    img = oracle.random_image(70, 45)
+    guide = oracle.random_u8(70 * 45 * 3)[::-1].copy().reshape(45, 70, 3)
+    got = _bilateral_gpu(dev, img, k, numerics=numerics, guide=guide)
+    want = oracle.joint_bilateral(img, guide, k, profile=profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("k", [3, 9, 15, 17, 31])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_adaptive(dev, oracle, k, numerics, profile):
+    img = oracle.random_image(50, 50)
+    h, w, _ = img.shape
+    f = vip.CudaAdaptiveBilateralFilter(w, h, k, numerics=numerics)
+    d_dst = dev.empty((h, w, 3))
+    f.execute(dev.put(img), d_dst)
+    got, want = dev.get(d_dst), oracle.adaptive(img, k, profile=profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+def test_adaptive_natural_image(dev, oracle, lenna):
+    h, w, _ = lenna.shape
+    f = vip.CudaAdaptiveBilateralFilter(w, h, 15)
+    d_dst = dev.empty((h, w, 3))
+    f.execute(dev.put(lenna), d_dst)
+    got, want = dev.get(d_dst), oracle.adaptive(lenna, 15, threads=16)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("ch", [1, 3])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_gradient(dev, oracle, ch, numerics, profile):
+    for src in (oracle.random_u8(2500 * ch).reshape(50, 50, ch), oracle.random_f32(2500 * ch).reshape(50, 50, ch)):
+        d_dst = dev.empty((50, 50), np.float32)
+        vip.cuda_gradient(dev.put(src), d_dst, 50, 50, ch, numerics=numerics)
+        got, want = dev.get(d_dst), oracle.gradient(src, profile)
+        assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("k", [5, 9])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_texture_stages_reference_inputs(dev, oracle, k, numerics, profile):
+    """test/bilateral_texture_filter.cu:386-461 inputs; blur/rtv bit-exact, guide exact."""
+    img = oracle.random_image(50, 50)
+    mag = oracle.random_f32(2500).reshape(50, 50)
+    t = _TextureImpl(50, 50, k, 1, numerics)
+    d_b, d_r = dev.empty((50, 50, 3), np.float32), dev.empty((50, 50), np.float32)
+    t.compute_blur_and_rtv(dev.put(img), dev.put(mag), d_b, d_r)
+    wb, wr = oracle.blur_rtv(img, mag, k, profile)
+    assert np.array_equal(dev.get(d_b), wb)
+    assert np.array_equal(dev.get(d_r), wr)
+    blurred = oracle.random_f32(7500).reshape(50, 50, 3)
+    rtv = oracle.random_f32(2500, 1.0).reshape(50, 50)
+    d_g = dev.empty((50, 50, 3))
+    t.compute_guide(dev.put(blurred), dev.put(rtv), d_g)
+    got, want = dev.get(d_g), oracle.guide(blurred, rtv, k, profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("shape,k,nitr", [((48, 64), 5, 5), ((50, 50), 9, 3), ((121, 203), 5, 3), ((7, 9), 3, 2)])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_texture_end_to_end(dev, oracle, shape, k, nitr, numerics, profile):
+    h, w = shape
+    img = oracle.random_u8(h * w * 3).reshape(h, w, 3)
+    f = vip.CudaBilateralTextureFilter(w, h, k, nitr, numerics=numerics)
+    d_dst = dev.empty((h, w, 3))
+    f.execute(dev.put(img), d_dst)
+    got, want = dev.get(d_dst), oracle.texture(img, k, nitr, profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+def test_texture_in_place_and_zero_iterations(dev, oracle):
+    img = oracle.random_image(40, 30)
+    f = vip.CudaBilateralTextureFilter(40, 30, 5, 1)
+    d = dev.put(img)
+    f.execute(d, d)  # src == dst is allowed (the reference copied first)
+    assert np.array_equal(dev.get(d), oracle.texture(img, 5, 1))
+    f0 = vip.CudaBilateralTextureFilter(40, 30, 5, 0)
+    d_dst = dev.empty((30, 40, 3))
+    f0.execute(dev.put(img), d_dst)
+    assert np.array_equal(dev.get(d_dst), img)
+
+
+def test_lenna_c1_bilateral(dev, oracle, goldens, lenna):
+    """BASELINE config C1 (bilateral r=5 on lenna) through the GPU path, both profiles."""
+    import hashlib
+    for numerics, tag in ((0, "cuda"), (1, "cpp")):
+        got = _bilateral_gpu(dev, lenna, 11, numerics=numerics)
+        sha = np.frombuffer(hashlib.sha256(got.tobytes()).digest(), np.uint8)
+        assert np.array_equal(sha, goldens[f"lenna_bilateral_{tag}_k11_sha256"])
+
+
+def test_row_band_api_matches_full_frame(dev, oracle):
+    """vip_bilateral_run_rows on a band with clamped halo == those rows of the frame."""
+    img = oracle.random_image(200, 90)
+    full = oracle.bilateral(img, 15)
+    impl = _BilateralImpl(200, 90, 15)
+    r = 7
+    for (b0, b1) in ((0, 30), (30, 61), (61, 90)):
+        lo, hi = max(b0 - r, 0), min(b1 + r, 90)
+        slab = dev.put(img[lo:hi])
+        out = dev.empty((b1 - b0, 200, 3))
+        impl.run_rows(slab, out, b1 - b0, b0 - lo, 0, hi - lo)
+        assert np.array_equal(dev.get(out), full[b0:b1])
+    ada = _AdaptiveImpl(200, 90, 15)
+    afull = oracle.adaptive(img, 15)
+    slab = dev.put(img[23:77])
+    out = dev.empty((40, 200, 3))
+    ada.run_rows(slab, out, 40, 7, 0, 54)
+    assert np.array_equal(dev.get(out), afull[30:70])
+
+
+def test_pitched_buffers(dev, oracle):
+    """The C ABI takes row pitches; the reference's dense API is pitch = width*3."""
+    import ctypes
+    img = oracle.random_image(100, 40)
+    pitch = 512
+    src = np.zeros((40, pitch), np.uint8)
+    src[:, :300] = img.reshape(40, 300)
+    d_src, d_dst = dev.put(src), dev.empty((40, pitch))
+    impl = _BilateralImpl(100, 40, 9)
+    vip.lib()  # loaded
+    from various_image_processings_amd._lib import call
+    call("vip_bilateral_run", impl._h, d_src.data_ptr(), pitch, d_dst.data_ptr(), pitch, None)
+    got = dev.get(d_dst)[:, :300].reshape(40, 100, 3)
+    assert np.array_equal(got, oracle.bilateral(img, 9))
+
+
+def test_argument_errors(dev):
+    with pytest.raises(vip.VipError) as e:
+        vip.CudaBilateralFilter(10, 10, 8)
+    assert e.value.code == 10002
+    with pytest.raises(vip.VipError):
+        vip.CudaBilateralFilter(10, 10, 33)
+    f = vip.CudaBilateralFilter(10, 10, 3)
+    d = dev.empty((10, 10, 3))
+    with pytest.raises(vip.VipError) as e:
+        f.bilateral_filter(d, d)
+    assert e.value.code == 10003
+
+
+def test_full_4k_frame_rows_exact(dev, oracle):
+    """C2 frame size (3840x2160, r=7): exact on rows spanning both borders and tile seams."""
+    img = oracle.random_image(3840, 2160)
+    got = _bilateral_gpu(dev, img, 15)
+    for r0 in (0, 5, 63, 64, 1000, 2151):
+        rows = min(9, 2160 - r0)
+        want = oracle.bilateral_rows(img, r0, rows, 15)
+        assert np.array_equal(got[r0:r0 + rows], want), (r0, _mismatch(got[r0:r0 + rows], want))
+
+
+def test_profiles_within_reference_tolerance(dev, oracle, lenna):
+    """GPU CUDA-profile output vs the include/cpp restatement: within the reference
+    tests' +-1 (EXPECT_NEAR(...,1)); report the exact-match fraction."""
+    got = _bilateral_gpu(dev, lenna, 15, numerics=0).astype(int)
+    want = oracle.bilateral(lenna, 15, profile=1, threads=16).astype(int)
+    diff = np.abs(got - want)
+    assert diff.max() <= 1
+    print(f"exact-match fraction vs include/cpp numerics: {(diff == 0).mean():.6f}")

@@ -1,0 +1,178 @@
+"""CPU tests of the oracle (test infrastructure): pinned inputs, regression
+goldens, and an independent numpy restatement on small cases."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+@pytest.mark.parametrize("name,kind,n,mx", [
+    ("random_array_u8_7500_255.bin", "u8", 7500, 255),
+    ("random_array_u8_2500_255.bin", "u8", 2500, 255),
+    ("random_array_f32_2500_255.bin", "f32", 2500, 255.0),
+    ("random_array_f32_7500_255.bin", "f32", 7500, 255.0),
+    ("random_array_f32_2500_1.bin", "f32", 2500, 1.0),
+])
+def test_input_generator_pinned_to_reference(oracle, name, kind, n, mx):
+    """oracle mt19937 == the reference's test/random_array.hpp (compiled in place)."""
+    ref = open(os.path.join(GOLDEN, name), "rb").read()
+    if kind == "u8":
+        assert np.array_equal(np.frombuffer(ref, np.uint8), oracle.random_u8(n, mx))
+    else:
+        assert np.array_equal(np.frombuffer(ref, np.float32), oracle.random_f32(n, mx))
+
+
+def test_oracle_regression_goldens(oracle, goldens, lenna):
+    import hashlib
+    img = oracle.random_image(50, 50)
+    for prof, tag in ((oracle.CUDA, "cuda"), (oracle.CPP, "cpp")):
+        for k in (3, 9, 11, 15, 31):
+            assert np.array_equal(goldens[f"bilateral_{tag}_k{k}"], oracle.bilateral(img, k, 10.0, 30.0, prof))
+            assert np.array_equal(goldens[f"adaptive_{tag}_k{k}"], oracle.adaptive(img, k, 10.0, 30.0, prof))
+        sha = hashlib.sha256(oracle.bilateral(lenna, 11, 10.0, 30.0, prof, threads=4).tobytes()).digest()
+        assert np.array_equal(goldens[f"lenna_bilateral_{tag}_k11_sha256"], np.frombuffer(sha, np.uint8))
+        assert np.array_equal(goldens[f"texture_{tag}_k5_n5"], oracle.texture(oracle.random_image(64, 48), 5, 5, prof))
+
+
+def test_threaded_oracle_equals_serial(oracle):
+    img = oracle.random_image(97, 61)
+    assert np.array_equal(oracle.bilateral(img, 11, threads=1), oracle.bilateral(img, 11, threads=5))
+    assert np.array_equal(oracle.adaptive(img, 9, threads=1), oracle.adaptive(img, 9, threads=3))
+
+
+def test_constant_image_is_fixed_point(oracle):
+    c = np.full((13, 21, 3), (17, 200, 99), np.uint8)
+    for prof in (oracle.CUDA, oracle.CPP):
+        assert np.array_equal(oracle.bilateral(c, 9, profile=prof), c)
+        assert np.array_equal(oracle.adaptive(c, 9, profile=prof), c)
+        assert np.array_equal(oracle.texture(c, 5, 2, profile=prof), c)
+
+
+def test_profiles_agree_within_one(oracle, lenna):
+    """The reference's own GPU path (float LUT + fma) and CPU path (double LUT,
+    mul+add) agree within the +-1 its tests allow (test/bilateral_filter.cu:58-60)."""
+    crop = lenna[200:280, 200:300]
+    for fn in (oracle.bilateral, oracle.adaptive):
+        a = fn(crop, 11, profile=oracle.CUDA).astype(int)
+        b = fn(crop, 11, profile=oracle.CPP).astype(int)
+        assert np.abs(a - b).max() <= 1
+
+
+# ---------------------------------------------------------------------------
+# Independent numpy restatement (float32 arithmetic in the reference's order)
+# cross-checks the C transcription on small images.
+# ---------------------------------------------------------------------------
+def _np_luts(ksize, ss, sc, n, profile):
+    r = ksize // 2
+    two_ss = np.float32(2) * np.float32(ss) * np.float32(ss)
+    two_sc = np.float32(2) * np.float32(sc) * np.float32(sc)
+    ky, kx = np.mgrid[-r:r + 1, -r:r + 1]
+    r2 = kx * kx + ky * ky
+    i = np.arange(n)
+    if profile == 1:
+        space = np.exp(r2.astype(np.float64) * (-1.0 / np.float64(two_ss))).astype(np.float32)
+        color = np.exp((i * i).astype(np.float64) * (-1.0 / np.float64(two_sc))).astype(np.float32)
+    else:
+        space = np.exp(r2.astype(np.float32) * (np.float32(-1) / two_ss)).astype(np.float32)
+        color = np.exp((i * i).astype(np.float32) * (np.float32(-1) / two_sc)).astype(np.float32)
+    space[r2 > r * r] = 0
+    return space, color
+
+
+def _np_bilateral_cpp(src, ksize, ss=10.0, sc=30.0, guide=None):
+    """include/cpp/bilateral_filter.hpp:76-104 in numpy float32, profile CPP."""
+    g = src if guide is None else guide
+    h, w, _ = src.shape
+    r = ksize // 2
+    space, color = _np_luts(ksize, ss, sc, 768, 1)
+    s = np.zeros((h, w, 3), np.float32)
+    sk = np.zeros((h, w), np.float32)
+    ys, xs = np.arange(h), np.arange(w)
+    for ky in range(-r, r + 1):
+        yc = np.clip(ys + ky, 0, h - 1)
+        for kx in range(-r, r + 1):
+            xc = np.clip(xs + kx, 0, w - 1)
+            nb = src[yc][:, xc].astype(np.float32)
+            gq = g[yc][:, xc].astype(np.int32)
+            d = np.abs(g.astype(np.int32) - gq).sum(axis=2)
+            wgt = (space[ky + r, kx + r] * color[d]).astype(np.float32)
+            s = (s + nb * wgt[..., None]).astype(np.float32)
+            sk = (sk + wgt).astype(np.float32)
+    return (s / sk[..., None] + np.float32(0.5)).astype(np.float32).astype(np.int32).astype(np.uint8)
+
+
+def test_numpy_restatement_bilateral_cpp(oracle):
+    img = oracle.random_image(23, 17)
+    guide = oracle.random_image(17, 23).reshape(17, 23, 3)[:, ::-1].copy()
+    for k in (3, 9):
+        assert np.array_equal(_np_bilateral_cpp(img, k), oracle.bilateral(img, k, profile=oracle.CPP))
+        assert np.array_equal(_np_bilateral_cpp(img, k, guide=guide),
+                              oracle.joint_bilateral(img, guide, k, profile=oracle.CPP))
+
+
+def test_numpy_restatement_gradient(oracle):
+    for ch in (1, 3):
+        u8 = oracle.random_u8(40 * 30 * ch).reshape(30, 40, ch)
+        f = oracle.random_f32(40 * 30 * ch).reshape(30, 40, ch)
+        for a in (u8, f):
+            x = a.astype(np.float32)
+            xp = np.concatenate([x[:, 1:], x[:, -1:]], 1)
+            xm = np.concatenate([x[:, :1], x[:, :-1]], 1)
+            yp = np.concatenate([x[1:], x[-1:]], 0)
+            ym = np.concatenate([x[:1], x[:-1]], 0)
+            h, v = (xp - xm).astype(np.float32), (yp - ym).astype(np.float32)
+            # CPP profile: sum_c (h*h + v*v)
+            s = np.zeros(x.shape[:2], np.float32)
+            for c in range(ch):
+                s = (s + ((h[..., c] * h[..., c]).astype(np.float32) + (v[..., c] * v[..., c]).astype(np.float32))
+                     ).astype(np.float32)
+            assert np.array_equal(np.sqrt(s), oracle.gradient(a, profile=oracle.CPP))
+
+
+def test_numpy_restatement_blur_rtv_guide(oracle):
+    img = oracle.random_image(31, 19)
+    mag = oracle.random_f32(31 * 19).reshape(19, 31)
+    k, r = 5, 2
+    b, rtv = oracle.blur_rtv(img, mag, k, oracle.CUDA)
+    h, w = mag.shape
+    ys, xs = np.arange(h), np.arange(w)
+    s = np.zeros((h, w, 3), np.float32)
+    imax = np.zeros((h, w), np.float32)
+    imin = np.full((h, w), 256, np.float32)
+    mmax = np.zeros((h, w), np.float32)
+    msum = np.zeros((h, w), np.float32)
+    for ky in range(-r, r + 1):
+        yc = np.clip(ys + ky, 0, h - 1)
+        for kx in range(-r, r + 1):
+            xc = np.clip(xs + kx, 0, w - 1)
+            p = img[yc][:, xc]
+            s = (s + p.astype(np.float32)).astype(np.float32)
+            inten = (p.astype(np.int32).sum(2).astype(np.float32) / np.float32(3)).astype(np.float32)
+            imax, imin = np.maximum(imax, inten), np.minimum(imin, inten)
+            m = mag[yc][:, xc]
+            mmax = np.maximum(mmax, m)
+            msum = (msum + m).astype(np.float32)
+    assert np.array_equal(b, (s / np.float32(k * k)).astype(np.float32))
+    num = ((imax - imin) * mmax).astype(np.float32)
+    assert np.array_equal(rtv, (num.astype(np.float64) / (msum.astype(np.float64) + 1e-9)).astype(np.float32))
+    # guide: first strict argmin, alpha blend with fma (profile CUDA)
+    g = oracle.guide(b, rtv, k, oracle.CUDA)
+    sa = np.float32(1) / np.float32(5 * k)
+    for y in range(h):
+        for x in range(w):
+            best, by, bx = np.float32(1e10), 0, 0
+            for ky in range(-r, r + 1):
+                for kx in range(-r, r + 1):
+                    yy, xx = min(max(y + ky, 0), h - 1), min(max(x + kx, 0), w - 1)
+                    if best > rtv[yy, xx]:
+                        best, by, bx = rtv[yy, xx], yy, xx
+            e = np.float32(np.exp(np.float64(np.float32(sa * np.float32(rtv[y, x] - best)))))
+            alpha = np.float32(np.float32(2) / np.float32(1 + e)) - np.float32(1)
+            beta = np.float32(1) - alpha
+            for c in range(3):
+                prod = np.float64(beta * b[y, x, c]).astype(np.float32)
+                v = np.float32(np.float64(alpha) * np.float64(b[by, bx, c]) + np.float64(prod))  # exact fma
+                v = np.float32(v + np.float32(0.5))
+                assert g[y, x, c] == min(max(int(v), 0), 255), (y, x, c)

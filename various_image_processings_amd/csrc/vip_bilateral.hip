@@ -1,0 +1,154 @@
+// Bilateral and joint-bilateral filter kernels for gfx950 (MI355X).
+//
+// Behaviour follows src/bilateral_filter_impl.cu:7-202 of the reference
+// (yuyuyu-bot/various_image_processings): per output pixel and per tap in
+// row-major order, w = ws[ky,kx] * wc[|db|+|dg|+|dr|], sum_c += p_c * w,
+// sumk += w, dst_c = u8(sum_c / sumk + 0.5f), replicate border. Taps outside
+// the disc carry an exact zero weight in the reference and are skipped here,
+// which leaves every sum bit-identical (x + 0*p == x).
+//
+// MI355X design: the kernel is FP32-VALU bound, not HBM bound,
+// so everything is arranged to minimise VALU instructions per (output, tap):
+//   v_sad_u8 (colour L1 distance of packed RGBX) -> v_lshl_or (LUT address)
+//   -> ds_read_b32 (32-copy LUT, bank-conflict free) -> v_mul (spatial weight
+//   from an SGPR) -> 3 x v_fma + v_add.
+// Neighbour pixels are read once per thread-row with ds_read_b128 and shared by
+// the thread's 8 horizontally adjacent outputs.
+#include "vip_stencil.hpp"
+
+namespace vip {
+
+template <int R, int WAVES, bool JOINT, bool FMA>
+__global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
+    using G = Geom<R>;
+    constexpr int NT = WAVES * 64;
+    constexpr int TH = WAVES * 4;
+    constexpr int ROWS = TH + 2 * R;
+    constexpr int PLANE = ROWS * G::S;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* const lut = lds;
+    uint32_t* const gplane = lds + lut_words(false);
+    uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
+
+    const int tile = blockIdx.x;
+    const int tx0 = (tile % a.tiles_x) * kTW;
+    const int ty0 = (tile / a.tiles_x) * TH;
+
+    stage_lut<NT, 768>(lut, a.color);
+    stage_plane<R, ROWS, NT>(gplane, a.guide, a.guide_pitch, a, tx0, ty0);
+    if constexpr (JOINT) stage_plane<R, ROWS, NT>(splane, a.src, a.src_pitch, a, tx0, ty0);
+    __syncthreads();
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int tx = lane & 15;
+    const int ty = (tid >> 6) * 4 + (lane >> 4);
+    const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+    const char* const lut_bytes = reinterpret_cast<const char*>(lut);
+
+    // centre pixels of the guide (== src for the plain filter)
+    uint32_t ctr[kP];
+    {
+        const uint32_t* c = gplane + (ty + R) * G::S + tx * kP + G::L;
+        const uint4 c0 = *reinterpret_cast<const uint4*>(c);
+        const uint4 c1 = *reinterpret_cast<const uint4*>(c + 4);
+        ctr[0] = c0.x; ctr[1] = c0.y; ctr[2] = c0.z; ctr[3] = c0.w;
+        ctr[4] = c1.x; ctr[5] = c1.y; ctr[6] = c1.z; ctr[7] = c1.w;
+    }
+    float s0[kP], s1[kP], s2[kP], sk[kP];
+#pragma unroll
+    for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
+
+    for (int ky = -R; ky <= R; ++ky) {
+        const int aky = ky < 0 ? -ky : ky;
+        const int hw = circle_hw(R, aky);
+        const int row_off = (ty + R + ky) * G::S + tx * kP;
+        const float* const ws = a.ws + aky * kWsStride;
+        HwDispatch<R, 0>::run(hw, [&](auto hwc) {
+            constexpr int HW = decltype(hwc)::value;
+            constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
+            constexpr int NC = C1 - C0 + 1;
+            uint32_t gp[4 * NC];
+            uint32_t sp[4 * NC];
+            load_row<C0, NC>(gplane, row_off, gp);
+            if constexpr (JOINT) load_row<C0, NC>(splane, row_off, sp);
+            else {
+#pragma unroll
+                for (int q = 0; q < 4 * NC; ++q) sp[q] = gp[q];
+            }
+            float wsv[HW + 1];
+#pragma unroll
+            for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
+            // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*32 + (lane & 31)
+            auto widx = [&](uint32_t g, float, float, float, int i) {
+                return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << 7) | lane4;
+            };
+            row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, sp, wsv, lut_bytes, widx, s0, s1, s2, sk);
+        });
+    }
+
+    uint32_t o[kP];
+#pragma unroll
+    for (int i = 0; i < kP; ++i) {
+        o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) | (f2u8(s2[i] / sk[i] + 0.5f) << 16);
+    }
+    store8(a, ty0 + ty, tx0 + tx * kP, o);
+}
+
+template <int R, bool JOINT, bool FMA>
+static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
+    constexpr int PLANES = JOINT ? 2 : 1;
+    constexpr int WAVES = pick_waves<R, PLANES>();
+    static_assert(WAVES > 0, "tile does not fit LDS");
+    constexpr int TH = WAVES * 4;
+    constexpr int LDS = lds_bytes<R, WAVES, PLANES>();
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA>;
+    static bool attr_done = false;  // benign race: idempotent attribute set
+    if (!attr_done) {
+        VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
+        attr_done = true;
+    }
+    const int tiles_y = (a.out_rows + TH - 1) / TH;
+    const int blocks = a.tiles_x * tiles_y;
+    if (blocks == 0) return 0;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, a);
+    return (int)hipGetLastError();
+}
+
+template <bool JOINT, bool FMA>
+static int launch_bilateral_dispatch(int radius, const StencilArgs& a, hipStream_t stream) {
+    switch (radius) {
+#define VIP_CASE(RR) \
+    case RR: return launch_bilateral_r<RR, JOINT, FMA>(a, stream);
+#ifdef VIP_ONLY_R7
+        VIP_CASE(7)
+#else
+        VIP_CASE(1) VIP_CASE(2) VIP_CASE(3) VIP_CASE(4) VIP_CASE(5) VIP_CASE(6) VIP_CASE(7) VIP_CASE(8)
+        VIP_CASE(9) VIP_CASE(10) VIP_CASE(11) VIP_CASE(12) VIP_CASE(13) VIP_CASE(14) VIP_CASE(15)
+#endif
+#undef VIP_CASE
+        default: return VIP_ERR_UNSUPPORTED_KSIZE;
+    }
+}
+
+// One translation unit per (JOINT, FMA) variant so the 15 radii compile in parallel.
+#if defined(VIP_BIL_JOINT) && defined(VIP_BIL_FMA)
+int launch_bilateral_joint_fma(int radius, const StencilArgs& a, hipStream_t s) {
+    return launch_bilateral_dispatch<true, true>(radius, a, s);
+}
+#elif defined(VIP_BIL_JOINT)
+int launch_bilateral_joint_mul(int radius, const StencilArgs& a, hipStream_t s) {
+    return launch_bilateral_dispatch<true, false>(radius, a, s);
+}
+#elif defined(VIP_BIL_FMA)
+int launch_bilateral_plain_fma(int radius, const StencilArgs& a, hipStream_t s) {
+    return launch_bilateral_dispatch<false, true>(radius, a, s);
+}
+#else
+int launch_bilateral_plain_mul(int radius, const StencilArgs& a, hipStream_t s) {
+    return launch_bilateral_dispatch<false, false>(radius, a, s);
+}
+#endif
+
+}  // namespace vip

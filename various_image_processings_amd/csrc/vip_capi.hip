@@ -1,0 +1,351 @@
+// extern "C" ABI of the MI355X bilateral-filter family (include/vip.h).
+//
+// Host-side responsibilities mirror the reference's Impl constructors
+// (src/bilateral_filter_impl.cu:204-239, src/adaptive_bilateral_filter_impl.cu:117-152,
+// src/bilateral_texture_filter_impl.cu:179-195): build the spatial and colour
+// LUTs once per handle, own device scratch, validate arguments. Unlike the
+// reference, run functions are asynchronous on the caller's stream and return a
+// status instead of printing it.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "vip_stencil.hpp"
+
+namespace vip {
+int launch_bilateral_joint_fma(int radius, const StencilArgs& a, hipStream_t s);
+int launch_bilateral_joint_mul(int radius, const StencilArgs& a, hipStream_t s);
+int launch_bilateral_plain_fma(int radius, const StencilArgs& a, hipStream_t s);
+int launch_bilateral_plain_mul(int radius, const StencilArgs& a, hipStream_t s);
+int launch_adaptive_fma(int radius, const StencilArgs& a, hipStream_t s);
+int launch_adaptive_mul(int radius, const StencilArgs& a, hipStream_t s);
+
+static int launch_bilateral(int radius, bool joint, bool fma, const StencilArgs& a, hipStream_t s) {
+    if (joint) return fma ? launch_bilateral_joint_fma(radius, a, s) : launch_bilateral_joint_mul(radius, a, s);
+    return fma ? launch_bilateral_plain_fma(radius, a, s) : launch_bilateral_plain_mul(radius, a, s);
+}
+static int launch_adaptive(int radius, bool fma, const StencilArgs& a, hipStream_t s) {
+    return fma ? launch_adaptive_fma(radius, a, s) : launch_adaptive_mul(radius, a, s);
+}
+int launch_gradient_u8(const uint8_t* src, float* dst, int width, int height, int ch, hipStream_t stream);
+int launch_gradient_f32(const float* src, float* dst, int width, int height, int ch, bool fma, hipStream_t stream);
+int launch_blur_rtv(const uint8_t* img, const float* mag, float* blurred, float* rtv, int width, int height,
+                    int ksize, bool cpp, hipStream_t stream);
+int launch_guide(const float* blurred, const float* rtv, uint8_t* guide, int width, int height, int ksize, bool cpp,
+                 hipStream_t stream);
+
+// LUT construction. CUDA profile: src/bilateral_filter_impl.cu:217-237 (float
+// coefficient, std::exp(float) == expf). CPP profile: include/cpp/bilateral_filter.hpp:13-36
+// (double coefficient, exp, stored as float). `2 * sigma * sigma` is a float
+// expression in both.
+static void build_space_q(int radius, float sigma_space, int numerics, float* wsq /* kWsStride^2 */) {
+    const float two_s2 = 2 * sigma_space * sigma_space;
+    const float cf = -1.f / two_s2;
+    const double cd = -1. / (double)two_s2;
+    for (int i = 0; i < kWsStride * kWsStride; ++i) wsq[i] = 0.f;
+    for (int ky = 0; ky <= radius; ++ky)
+        for (int kx = 0; kx <= radius; ++kx) {
+            const int r2 = kx * kx + ky * ky;
+            if (r2 > radius * radius) continue;
+            wsq[ky * kWsStride + kx] =
+                numerics == VIP_NUMERICS_CPP ? (float)std::exp((double)r2 * cd) : expf((float)r2 * cf);
+        }
+}
+
+static void build_color(int len, float sigma_color, int numerics, float* out) {
+    const float two_s2 = 2 * sigma_color * sigma_color;
+    const float cf = -1.f / two_s2;
+    const double cd = -1. / (double)two_s2;
+    for (int i = 0; i < len; ++i)
+        out[i] = numerics == VIP_NUMERICS_CPP ? (float)std::exp((double)(i * i) * cd) : expf((float)(i * i) * cf);
+}
+
+static bool valid_ksize(int ksize) { return ksize >= 3 && (ksize & 1) && ksize / 2 <= kMaxRadius; }
+
+static int upload_color(float** d_color, int len, float sigma_color, int numerics) {
+    float host[1536];
+    build_color(len, sigma_color, numerics, host);
+    VIP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(d_color), sizeof(float) * len));
+    VIP_HIP_CHECK(hipMemcpy(*d_color, host, sizeof(float) * len, hipMemcpyHostToDevice));
+    return 0;
+}
+
+static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_pitch, const uint8_t* guide,
+                      size_t guide_pitch, uint8_t* dst, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
+                      int row_hi, const float* d_color, const float* wsq) {
+    a.src = src;
+    a.guide = guide;
+    a.dst = dst;
+    a.src_pitch = (long long)src_pitch;
+    a.guide_pitch = (long long)guide_pitch;
+    a.dst_pitch = (long long)dst_pitch;
+    a.width = width;
+    a.out_rows = out_rows;
+    a.src_row0 = src_row0;
+    a.row_lo = row_lo;
+    a.row_hi = row_hi;
+    a.tiles_x = (width + kTW - 1) / kTW;
+    const auto al4 = [](const void* p, size_t pitch) { return ((uintptr_t)p % 4 == 0) && (pitch % 4 == 0); };
+    a.aligned = al4(src, src_pitch) && al4(guide, guide_pitch);
+    a.dst_aligned = ((uintptr_t)dst % 8 == 0) && (dst_pitch % 8 == 0);
+    a.color = d_color;
+    std::memcpy(a.ws, wsq, sizeof(a.ws));
+}
+
+}  // namespace vip
+
+using namespace vip;
+
+struct vip_bilateral_s {
+    int width, height, ksize, radius, numerics;
+    float* d_color;
+    float wsq[kWsStride * kWsStride];
+};
+
+struct vip_adaptive_s {
+    int width, height, ksize, radius, numerics;
+    float* d_color;
+    float wsq[kWsStride * kWsStride];
+};
+
+struct vip_texture_s {
+    int width, height, ksize, nitr, numerics;
+    vip_bilateral_t jbf;
+    uint8_t* d_ping[2];
+    uint8_t* d_guide;
+    float* d_mag;
+    float* d_blurred;
+    float* d_rtv;
+};
+
+extern "C" {
+
+int vip_abi_version(void) { return VIP_ABI_VERSION; }
+int vip_max_radius(void) { return kMaxRadius; }
+
+const char* vip_error_string(int code) {
+    switch (code) {
+        case 0: return "success";
+        case VIP_ERR_INVALID_ARGUMENT: return "invalid argument";
+        case VIP_ERR_UNSUPPORTED_KSIZE: return "unsupported ksize (must be odd, 3..31)";
+        case VIP_ERR_ALIASING: return "source and destination alias";
+        default: return hipGetErrorString((hipError_t)code);
+    }
+}
+
+int vip_malloc(void** d_ptr, size_t bytes) {
+    if (!d_ptr) return VIP_ERR_INVALID_ARGUMENT;
+    return (int)hipMalloc(d_ptr, bytes);
+}
+int vip_free(void* d_ptr) { return (int)hipFree(d_ptr); }
+int vip_upload(void* d_dst, const void* h_src, size_t bytes) {
+    return (int)hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice);
+}
+int vip_download(void* h_dst, const void* d_src, size_t bytes) {
+    return (int)hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost);
+}
+int vip_device_synchronize(void) { return (int)hipDeviceSynchronize(); }
+int vip_stream_synchronize(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
+
+// ---------------------------------------------------------------- bilateral
+int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
+                         int numerics) {
+    if (!out || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
+    if (!valid_ksize(ksize)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    auto* h = new (std::nothrow) vip_bilateral_s();
+    if (!h) return (int)hipErrorOutOfMemory;
+    h->width = width;
+    h->height = height;
+    h->ksize = ksize;
+    h->radius = ksize / 2;
+    h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
+    build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
+    const int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics);
+    if (rc) {
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int vip_bilateral_destroy(vip_bilateral_t h) {
+    if (!h) return 0;
+    const int rc = (int)hipFree(h->d_color);
+    delete h;
+    return rc;
+}
+
+int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
+                           size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, int out_rows, int src_row0,
+                           int row_lo, int row_hi, void* stream) {
+    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+    if (d_dst == d_src || (d_guide && d_dst == d_guide)) return VIP_ERR_ALIASING;
+    const bool joint = d_guide != nullptr;
+    StencilArgs a;
+    fill_args(a, h->width, d_src, src_pitch, joint ? d_guide : d_src, joint ? guide_pitch : src_pitch, d_dst,
+              dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->wsq);
+    return launch_bilateral(h->radius, joint, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
+}
+
+int vip_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
+                      void* stream) {
+    if (!h) return VIP_ERR_INVALID_ARGUMENT;
+    return vip_bilateral_run_rows(h, d_src, src_pitch, nullptr, 0, d_dst, dst_pitch, h->height, 0, 0, h->height,
+                                  stream);
+}
+
+int vip_joint_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
+                            size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, void* stream) {
+    if (!h || !d_guide) return VIP_ERR_INVALID_ARGUMENT;
+    return vip_bilateral_run_rows(h, d_src, src_pitch, d_guide, guide_pitch, d_dst, dst_pitch, h->height, 0, 0,
+                                  h->height, stream);
+}
+
+// ---------------------------------------------------------------- adaptive
+int vip_adaptive_create(vip_adaptive_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
+                        int numerics) {
+    if (!out || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
+    if (!valid_ksize(ksize)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    auto* h = new (std::nothrow) vip_adaptive_s();
+    if (!h) return (int)hipErrorOutOfMemory;
+    h->width = width;
+    h->height = height;
+    h->ksize = ksize;
+    h->radius = ksize / 2;
+    h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
+    build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
+    // the reference's table is 512*3 long (src/adaptive_bilateral_filter_impl.cu:5)
+    const int rc = upload_color(&h->d_color, 1536, sigma_color, h->numerics);
+    if (rc) {
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int vip_adaptive_destroy(vip_adaptive_t h) {
+    if (!h) return 0;
+    const int rc = (int)hipFree(h->d_color);
+    delete h;
+    return rc;
+}
+
+int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
+                          int out_rows, int src_row0, int row_lo, int row_hi, void* stream) {
+    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+    if (d_dst == d_src) return VIP_ERR_ALIASING;
+    StencilArgs a;
+    fill_args(a, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo, row_hi,
+              h->d_color, h->wsq);
+    return launch_adaptive(h->radius, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
+}
+
+int vip_adaptive_run(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
+                     void* stream) {
+    if (!h) return VIP_ERR_INVALID_ARGUMENT;
+    return vip_adaptive_run_rows(h, d_src, src_pitch, d_dst, dst_pitch, h->height, 0, 0, h->height, stream);
+}
+
+// ---------------------------------------------------------------- gradient
+int vip_gradient_u8(const uint8_t* d_src, float* d_dst, int width, int height, int src_ch, int numerics,
+                    void* stream) {
+    (void)numerics;  // u8 arithmetic is exact in both profiles
+    if (!d_src || !d_dst || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
+    return launch_gradient_u8(d_src, d_dst, width, height, src_ch, (hipStream_t)stream);
+}
+
+int vip_gradient_f32(const float* d_src, float* d_dst, int width, int height, int src_ch, int numerics,
+                     void* stream) {
+    if (!d_src || !d_dst || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
+    return launch_gradient_f32(d_src, d_dst, width, height, src_ch, numerics != VIP_NUMERICS_CPP,
+                               (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------- texture
+int vip_texture_destroy(vip_texture_t h) {
+    if (!h) return 0;
+    vip_bilateral_destroy(h->jbf);
+    (void)hipFree(h->d_ping[0]);
+    (void)hipFree(h->d_ping[1]);
+    (void)hipFree(h->d_guide);
+    (void)hipFree(h->d_mag);
+    (void)hipFree(h->d_blurred);
+    (void)hipFree(h->d_rtv);
+    delete h;
+    return 0;
+}
+
+int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int nitr, int numerics) {
+    if (!out || width <= 0 || height <= 0 || nitr < 0 || ksize < 1) return VIP_ERR_INVALID_ARGUMENT;
+    // the embedded JBF has ksize 2k-1 (src/bilateral_texture_filter_impl.cu:188)
+    if (!valid_ksize(2 * ksize - 1)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    auto* h = new (std::nothrow) vip_texture_s();
+    if (!h) return (int)hipErrorOutOfMemory;
+    h->width = width;
+    h->height = height;
+    h->ksize = ksize;
+    h->nitr = nitr;
+    h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
+    const size_t n = (size_t)width * height;
+    int rc = vip_bilateral_create(&h->jbf, width, height, 2 * ksize - 1, (float)(ksize - 1), 1.73205080757f,
+                                  h->numerics);
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_ping[0]), n * 3);
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_ping[1]), n * 3);
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_guide), n * 3);
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_mag), n * sizeof(float));
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_blurred), n * 3 * sizeof(float));
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_rtv), n * sizeof(float));
+    if (rc) {
+        vip_texture_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int vip_texture_blur_rtv(vip_texture_t h, const uint8_t* d_image, const float* d_magnitude, float* d_blurred,
+                         float* d_rtv, void* stream) {
+    if (!h || !d_image || !d_magnitude || !d_blurred || !d_rtv) return VIP_ERR_INVALID_ARGUMENT;
+    return launch_blur_rtv(d_image, d_magnitude, d_blurred, d_rtv, h->width, h->height, h->ksize,
+                           h->numerics == VIP_NUMERICS_CPP, (hipStream_t)stream);
+}
+
+int vip_texture_guide(vip_texture_t h, const float* d_blurred, const float* d_rtv, uint8_t* d_guide, void* stream) {
+    if (!h || !d_blurred || !d_rtv || !d_guide) return VIP_ERR_INVALID_ARGUMENT;
+    return launch_guide(d_blurred, d_rtv, d_guide, h->width, h->height, h->ksize, h->numerics == VIP_NUMERICS_CPP,
+                        (hipStream_t)stream);
+}
+
+// Impl::execute (src/bilateral_texture_filter_impl.cu:199-214) without the
+// nitr + 2 device-to-device copies: iteration i reads X_i and writes X_{i+1},
+// X_0 = d_src, X_nitr = d_dst, intermediates alternate between two scratch frames.
+int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream) {
+    if (!h || !d_src || !d_dst) return VIP_ERR_INVALID_ARGUMENT;
+    const hipStream_t s = (hipStream_t)stream;
+    const size_t bytes = (size_t)h->width * h->height * 3;
+    const size_t pitch = (size_t)h->width * 3;
+    if (h->nitr == 0) {
+        if (d_src != d_dst) VIP_HIP_CHECK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, s));
+        return 0;
+    }
+    const uint8_t* cur = d_src;
+    if (d_src == d_dst) {  // the last JBF must not write the frame it reads
+        VIP_HIP_CHECK(hipMemcpyAsync(h->d_ping[1], d_src, bytes, hipMemcpyDeviceToDevice, s));
+        cur = h->d_ping[1];
+    }
+    for (int it = 0; it < h->nitr; ++it) {
+        uint8_t* next = (it == h->nitr - 1) ? d_dst : (cur == h->d_ping[0] ? h->d_ping[1] : h->d_ping[0]);
+        int rc = launch_gradient_u8(cur, h->d_mag, h->width, h->height, 3, s);
+        if (!rc) rc = vip_texture_blur_rtv(h, cur, h->d_mag, h->d_blurred, h->d_rtv, stream);
+        if (!rc) rc = vip_texture_guide(h, h->d_blurred, h->d_rtv, h->d_guide, stream);
+        if (!rc) rc = vip_joint_bilateral_run(h->jbf, cur, pitch, h->d_guide, pitch, next, pitch, stream);
+        if (rc) return rc;
+        cur = next;
+    }
+    return 0;
+}
+
+}  // extern "C"

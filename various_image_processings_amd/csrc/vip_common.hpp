@@ -1,0 +1,47 @@
+// Shared device/host helpers for the MI355X (gfx950) bilateral-filter family.
+// Replaces src/device_utilities.cuh (clamp) and src/host_utilities.hpp
+// (CUDASafeCall) of the reference with a status-returning HIP layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+#include "vip.h"
+
+namespace vip {
+
+// Reference: src/device_utilities.cuh:5-10.
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// static_cast<uint8_t>(v) for v in [0, 256); v_cvt_i32_f32 maps NaN to 0.
+__device__ __forceinline__ uint32_t f2u8(float v) { return (uint32_t)(int)v & 0xffu; }
+
+// Round a launch-time size up to a multiple.
+constexpr int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+// Number of LUT copies interleaved in LDS so that the 32 lanes of a ds_read_b32
+// half-wave each hit their own bank (bank = (addr/4) % 32): entry d of copy c sits
+// at word d*32 + c, so lane l reads word d*32 + (l & 31) -> bank l & 31.
+constexpr int kLutCopies = 32;
+
+// Circle half-width of row ky for a disc of radius R: the largest |kx| with
+// kx^2 + ky^2 <= R^2 (src/bilateral_filter_impl.cu:222-231 masks the square LUT
+// with the same test, so taps outside it carry an exact zero weight).
+__host__ __device__ constexpr int isqrt_floor(int v) {
+    int r = 0;
+    while ((r + 1) * (r + 1) <= v) ++r;
+    return r;
+}
+__host__ __device__ constexpr int circle_hw(int R, int ky) { return isqrt_floor(R * R - ky * ky); }
+
+}  // namespace vip
+
+// Record the first error of a call; launch errors come back through
+// hipGetLastError (the reference printed them and carried on,
+// src/host_utilities.hpp:9-13; the C ABI returns them instead).
+#define VIP_HIP_CHECK(expr)                                  \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return (int)_e;                \
+    } while (0)

@@ -1,0 +1,232 @@
+// Tile geometry and kernel arguments shared by the bilateral, joint-bilateral and
+// adaptive-bilateral kernels (gfx950).
+//
+// Layout in LDS (one workgroup per CU):
+//   [0, 96 KiB)      colour LUT, 768 entries x 32 interleaved copies (word d*32 + c)
+//                    -> every ds_read_b32 half-wave is bank-conflict free.
+//                    The adaptive kernel uses 1536 entries x 16 copies (same 96 KiB).
+//   [96 KiB, ...)    RGBX tile plane(s): (TH + 2R) rows x S words, one u32 per pixel
+//                    (byte 3 = 0 so v_sad_u8 sees exactly |db|+|dg|+|dr|).
+//                    S = round_up(TW + 2L, 8) + 4 words (S = 4 mod 8): the 16 lanes of a
+//                    ds_read_b128 group land on disjoint banks.
+// Thread mapping: wave w covers tile rows 4w..4w+3, lane l -> row 4w + l/16, columns
+// 8*(l%16) .. 8*(l%16)+7 (P = 8 horizontally adjacent outputs per thread).
+#pragma once
+
+#include "vip_common.hpp"
+
+namespace vip {
+
+constexpr int kMaxRadius = 15;            // ksize <= 31 (BASELINE C5 uses ksize 31)
+constexpr int kWsStride = kMaxRadius + 1; // spatial weights stored as ws[|ky|][|kx|]
+constexpr int kP = 8;                     // outputs per thread
+constexpr int kTW = 16 * kP;              // tile width in pixels
+constexpr int kLdsBudget = 160 * 1024;
+
+struct StencilArgs {
+    const uint8_t* src;
+    const uint8_t* guide;  // == src for the plain filters
+    uint8_t* dst;
+    long long src_pitch, guide_pitch, dst_pitch;
+    int width;
+    int out_rows;          // output rows to produce
+    int src_row0;          // source row of output row 0
+    int row_lo, row_hi;    // neighbour rows clamp to [row_lo, row_hi)
+    int tiles_x;
+    int aligned;           // src/guide base and pitch are 4-byte aligned -> dword tile loads
+    int dst_aligned;       // dst base and pitch are 8-byte aligned -> qword stores
+    const float* color;    // colour LUT in device memory
+    float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
+};
+
+constexpr int lut_words(bool adaptive) { return adaptive ? 1536 * 16 : 768 * 32; }
+
+template <int R>
+struct Geom {
+    static constexpr int L = round_up(R, 4);               // left/right apron, 4-px aligned
+    static constexpr int S = round_up(kTW + 2 * L, 8) + 4;  // LDS row stride (words)
+    static constexpr int GROUPS = (kTW + 2 * L) / 4;        // 4-pixel groups per tile row
+};
+
+// Largest wave count (16, 8 or 4) whose LUT + plane(s) fit the CU's LDS.
+template <int R, int PLANES>
+constexpr int pick_waves() {
+    for (int w = 16; w >= 4; w /= 2) {
+        const long long bytes = 4LL * lut_words(false) + 4LL * PLANES * (w * 4 + 2 * R) * Geom<R>::S;
+        if (bytes <= kLdsBudget) return w;
+    }
+    return 0;
+}
+
+template <int R, int WAVES, int PLANES>
+constexpr int lds_bytes() {
+    return 4 * lut_words(false) + 4 * PLANES * (WAVES * 4 + 2 * R) * Geom<R>::S;
+}
+
+// Calls f(std::integral_constant<int, HW>) for the runtime circle half-width hw.
+// circle_hw is non-increasing in |ky|, so deduplicating neighbours instantiates
+// each distinct row body once.
+template <int R, int KY>
+struct HwDispatch {
+    template <class F>
+    __device__ __forceinline__ static void run(int hw, F&& f) {
+        constexpr int H = circle_hw(R, KY);
+        if constexpr (KY == 0 || circle_hw(R, KY - 1) != H) {
+            if (hw == H) {
+                f(std::integral_constant<int, H>{});
+                return;
+            }
+        }
+        if constexpr (KY < R) HwDispatch<R, KY + 1>::run(hw, static_cast<F&&>(f));
+    }
+};
+
+// 12 bytes (4 RGB pixels) -> 4 RGBX words.
+__device__ __forceinline__ uint4 unpack_rgb4(uint32_t a, uint32_t b, uint32_t c) {
+    uint4 r;
+    r.x = a & 0xffffffu;
+    r.y = __builtin_amdgcn_alignbyte(b, a, 3) & 0xffffffu;
+    r.z = __builtin_amdgcn_alignbyte(c, b, 2) & 0xffffffu;
+    r.w = c >> 8;
+    return r;
+}
+
+__device__ __forceinline__ uint32_t load_rgb(const uint8_t* row, int x) {
+    const uint8_t* p = row + 3 * x;
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
+}
+
+// Stage source rows [ty0 + src_row0 - R, ... + ROWS) x columns [tx0 - L, tx0 - L + TW + 2L)
+// of `img` into `plane`, clamping rows to [row_lo, row_hi) and columns to [0, width).
+template <int R, int ROWS, int NT>
+__device__ __forceinline__ void stage_plane(uint32_t* plane, const uint8_t* img, long long pitch, const StencilArgs& a,
+                                            int tx0, int ty0) {
+    using G = Geom<R>;
+    const int tid = threadIdx.x;
+    for (int g = tid; g < ROWS * G::GROUPS; g += NT) {
+        const int r = g / G::GROUPS;
+        const int gc = g - r * G::GROUPS;
+        const int sy = clampi(ty0 + a.src_row0 - R + r, a.row_lo, a.row_hi - 1);
+        const uint8_t* row = img + (long long)sy * pitch;
+        const int x = tx0 - G::L + 4 * gc;
+        uint4 q;
+        if (a.aligned && x >= 0 && x + 3 < a.width) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
+            q = unpack_rgb4(w[0], w[1], w[2]);
+        } else {
+            q.x = load_rgb(row, clampi(x + 0, 0, a.width - 1));
+            q.y = load_rgb(row, clampi(x + 1, 0, a.width - 1));
+            q.z = load_rgb(row, clampi(x + 2, 0, a.width - 1));
+            q.w = load_rgb(row, clampi(x + 3, 0, a.width - 1));
+        }
+        *reinterpret_cast<uint4*>(plane + r * G::S + 4 * gc) = q;
+    }
+}
+
+// Fill the interleaved colour LUT: word d*COPIES + c = color[d], for
+// 768 entries x 32 copies (bilateral) or 1536 x 16 (adaptive) = 96 KiB.
+template <int NT, int ENTRIES>
+__device__ __forceinline__ void stage_lut(uint32_t* lut, const float* color) {
+    constexpr int COPIES = 768 * 32 / ENTRIES;
+    constexpr int SHIFT = COPIES == 32 ? 3 : 2;  // (4 words per store) / COPIES
+    for (int q = threadIdx.x; q < 768 * 32 / 4; q += NT) {
+        const uint32_t v = __float_as_uint(color[q >> SHIFT]);
+        *reinterpret_cast<uint4*>(lut + 4 * q) = make_uint4(v, v, v, v);
+    }
+}
+
+// Load the 4*NC neighbour words of columns [4*C0, 4*C0 + 4*NC) of one tile row
+// (row_off is 16-byte aligned; indexing as uint4 lets hipcc emit ds_read_b128).
+template <int C0, int NC>
+__device__ __forceinline__ void load_row(const uint32_t* plane, int row_off, uint32_t (&w)[4 * NC]) {
+    const uint4* v = reinterpret_cast<const uint4*>(plane) + (row_off >> 2) + C0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint4 q = v[c];
+        w[4 * c + 0] = q.x; w[4 * c + 1] = q.y; w[4 * c + 2] = q.z; w[4 * c + 3] = q.w;
+    }
+}
+
+// The tap loop of one tile row for the thread's kP outputs, software-pipelined
+// one neighbour column ahead: while column j's weights are accumulated, column
+// j+1's colour-LUT reads are already in flight (the LDS latency is hidden inside
+// the wave instead of only across waves). `widx(g, f0, f1, f2, i)` returns the LDS
+// byte address of the colour weight of guide word g (source floats f*) for output i.
+// Accumulation order per output is ascending kx, as in the reference's row-major loop.
+template <int HW, int L, int C0, int NGP, bool FMA, class WIdx>
+__device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32_t (&sp)[NGP],
+                                         const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
+                                         float (&s0)[kP], float (&s1)[kP], float (&s2)[kP], float (&sk)[kP]) {
+    constexpr int J0 = L - HW;           // first neighbour column relative to the thread's 8
+    constexpr int J1 = L + kP - 1 + HW;  // last
+    float wc[2][kP];
+    float nf[2][3];
+    auto issue = [&](int j) {
+        const uint32_t g = gp[j - 4 * C0];
+        const uint32_t p = sp[j - 4 * C0];
+        float* f = nf[j & 1];
+        f[0] = (float)(p & 0xffu);
+        f[1] = (float)((p >> 8) & 0xffu);
+        f[2] = (float)((p >> 16) & 0xffu);
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+            const int kx = j - L - i;
+            if (kx < -HW || kx > HW) continue;
+            wc[j & 1][i] = *reinterpret_cast<const float*>(lut + widx(g, f[0], f[1], f[2], i));
+        }
+    };
+    issue(J0);
+#pragma unroll
+    for (int j = J0; j <= J1; ++j) {
+        if (j < J1) issue(j + 1);
+        const float* f = nf[j & 1];
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+            const int kx = j - L - i;
+            if (kx < -HW || kx > HW) continue;
+            const float w = wc[j & 1][i] * wsv[kx < 0 ? -kx : kx];
+            if constexpr (FMA) {
+                s0[i] = __builtin_fmaf(f[0], w, s0[i]);
+                s1[i] = __builtin_fmaf(f[1], w, s1[i]);
+                s2[i] = __builtin_fmaf(f[2], w, s2[i]);
+            } else {
+                s0[i] = s0[i] + f[0] * w;
+                s1[i] = s1[i] + f[1] * w;
+                s2[i] = s2[i] + f[2] * w;
+            }
+            sk[i] = sk[i] + w;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+}
+
+// Write 8 RGB outputs (24 bytes) of row oy starting at column x.
+__device__ __forceinline__ void store8(const StencilArgs& a, int oy, int x, const uint32_t (&o)[kP]) {
+    if (oy >= a.out_rows || x >= a.width) return;
+    uint8_t* row = a.dst + (long long)oy * a.dst_pitch;
+    if (a.dst_aligned && x + kP <= a.width) {
+        uint32_t w[6];
+        w[0] = o[0] | (o[1] << 24);
+        w[1] = (o[1] >> 8) | (o[2] << 16);
+        w[2] = (o[2] >> 16) | (o[3] << 8);
+        w[3] = o[4] | (o[5] << 24);
+        w[4] = (o[5] >> 8) | (o[6] << 16);
+        w[5] = (o[6] >> 16) | (o[7] << 8);
+        uint2* p = reinterpret_cast<uint2*>(row + 3 * x);
+        p[0] = make_uint2(w[0], w[1]);
+        p[1] = make_uint2(w[2], w[3]);
+        p[2] = make_uint2(w[4], w[5]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < kP; ++i) {
+            if (x + i < a.width) {
+                uint8_t* p = row + 3 * (x + i);
+                p[0] = (uint8_t)(o[i]);
+                p[1] = (uint8_t)(o[i] >> 8);
+                p[2] = (uint8_t)(o[i] >> 16);
+            }
+        }
+    }
+}
+
+}  // namespace vip

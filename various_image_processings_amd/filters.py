@@ -1,0 +1,226 @@
+"""Python mirror of the reference's include/cuda/*.hpp API, over the C ABI.
+
+Same class and method names, argument meaning and defaults as
+yuyuyu-bot/various_image_processings:
+
+* ``CudaBilateralFilter(width, height, ksize=9, sigma_space=10., sigma_color=30.)``
+  with ``bilateral_filter(d_src, d_dst)`` and ``joint_bilateral_filter(d_src, d_guide, d_dst)``
+  (include/cuda/bilateral_filter.hpp:9-24)
+* ``CudaAdaptiveBilateralFilter(...).execute(d_src, d_dst)`` (adaptive_bilateral_filter.hpp:9-19)
+* ``CudaBilateralTextureFilter(width, height, ksize=9, nitr=3).execute(d_src, d_dst)``
+  (bilateral_texture_filter.hpp:9-12)
+* ``cuda_gradient(d_src, d_dst, width, height, src_ch=1)`` (gradient.hpp:13-23)
+* ``DeviceImage(width, height, channels=1, dtype)`` with upload/download/get (device_image.hpp:4-16)
+
+Images are device buffers: a ``torch.Tensor`` on a HIP device (dense, uint8 for
+images, float32 for magnitude/blurred/rtv) or a raw device address (int). Public
+methods synchronise the device like the reference's; ``impl_`` exposes the
+non-synchronising calls the reference's tests drive, plus an optional ``stream``.
+Errors raise :class:`VipError` (the reference printed them and carried on).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+from . import _lib
+from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
+
+__all__ = [
+    "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
+    "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
+]
+
+
+def _ptr(buf) -> int:
+    """Device address of a torch tensor (checked dense) or an int address."""
+    if isinstance(buf, int):
+        return buf
+    if hasattr(buf, "data_ptr"):
+        if not buf.is_cuda:
+            raise ValueError("expected a device tensor (torch.cuda / HIP), got a host tensor")
+        if not buf.is_contiguous():
+            raise ValueError("expected a dense (contiguous) tensor")
+        return buf.data_ptr()
+    if isinstance(buf, DeviceImage):
+        return buf.get()
+    raise TypeError(f"cannot take a device pointer of {type(buf).__name__}")
+
+
+def _stream(stream) -> Optional[int]:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+def device_synchronize() -> None:
+    call("vip_device_synchronize")
+
+
+class _Handle:
+    _destroy = ""
+
+    def __init__(self):
+        self._h = ctypes.c_void_p()
+
+    def close(self) -> None:
+        if self._h and self._h.value:
+            getattr(lib(), self._destroy)(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _BilateralImpl(_Handle):
+    """CudaBilateralFilter::Impl (src/bilateral_filter_impl.cuh:7-33): no synchronisation."""
+    _destroy = "vip_bilateral_destroy"
+
+    def __init__(self, width, height, ksize=9, sigma_space=10.0, sigma_color=30.0, numerics=VIP_NUMERICS_CUDA):
+        super().__init__()
+        self.width, self.height, self.ksize = int(width), int(height), int(ksize)
+        call("vip_bilateral_create", ctypes.byref(self._h), self.width, self.height, self.ksize,
+             float(sigma_space), float(sigma_color), int(numerics))
+
+    def bilateral_filter(self, d_src, d_dst, stream=None):
+        p = self.width * 3
+        call("vip_bilateral_run", self._h, _ptr(d_src), p, _ptr(d_dst), p, _stream(stream))
+
+    def joint_bilateral_filter(self, d_src, d_guide, d_dst, stream=None):
+        p = self.width * 3
+        call("vip_joint_bilateral_run", self._h, _ptr(d_src), p, _ptr(d_guide), p, _ptr(d_dst), p, _stream(stream))
+
+    def run_rows(self, d_src, d_dst, out_rows, src_row0, row_lo, row_hi, d_guide=None, stream=None):
+        """Row-band filter for row-sharded frames (include/vip.h vip_bilateral_run_rows)."""
+        p = self.width * 3
+        g = None if d_guide is None else _ptr(d_guide)
+        call("vip_bilateral_run_rows", self._h, _ptr(d_src), p, g, p, _ptr(d_dst), p, int(out_rows), int(src_row0),
+             int(row_lo), int(row_hi), _stream(stream))
+
+
+class CudaBilateralFilter:
+    """include/cuda/bilateral_filter.hpp:7-29; public calls block until done (:299, :309)."""
+
+    def __init__(self, width, height, ksize=9, sigma_space=10.0, sigma_color=30.0, numerics=VIP_NUMERICS_CUDA):
+        self.impl_ = _BilateralImpl(width, height, ksize, sigma_space, sigma_color, numerics)
+
+    def bilateral_filter(self, d_src, d_dst):
+        self.impl_.bilateral_filter(d_src, d_dst)
+        device_synchronize()
+
+    def joint_bilateral_filter(self, d_src, d_guide, d_dst):
+        self.impl_.joint_bilateral_filter(d_src, d_guide, d_dst)
+        device_synchronize()
+
+
+class _AdaptiveImpl(_Handle):
+    """CudaAdaptiveBilateralFilter::Impl (src/adaptive_bilateral_filter_impl.cuh:7-29)."""
+    _destroy = "vip_adaptive_destroy"
+
+    def __init__(self, width, height, ksize=9, sigma_space=10.0, sigma_color=30.0, numerics=VIP_NUMERICS_CUDA):
+        super().__init__()
+        self.width, self.height, self.ksize = int(width), int(height), int(ksize)
+        call("vip_adaptive_create", ctypes.byref(self._h), self.width, self.height, self.ksize,
+             float(sigma_space), float(sigma_color), int(numerics))
+
+    def execute(self, d_src, d_dst, stream=None):
+        p = self.width * 3
+        call("vip_adaptive_run", self._h, _ptr(d_src), p, _ptr(d_dst), p, _stream(stream))
+
+    def run_rows(self, d_src, d_dst, out_rows, src_row0, row_lo, row_hi, stream=None):
+        p = self.width * 3
+        call("vip_adaptive_run_rows", self._h, _ptr(d_src), p, _ptr(d_dst), p, int(out_rows), int(src_row0),
+             int(row_lo), int(row_hi), _stream(stream))
+
+
+class CudaAdaptiveBilateralFilter:
+    """include/cuda/adaptive_bilateral_filter.hpp:7-24."""
+
+    def __init__(self, width, height, ksize=9, sigma_space=10.0, sigma_color=30.0, numerics=VIP_NUMERICS_CUDA):
+        self.impl_ = _AdaptiveImpl(width, height, ksize, sigma_space, sigma_color, numerics)
+
+    def execute(self, d_src, d_dst):
+        self.impl_.execute(d_src, d_dst)
+        device_synchronize()
+
+
+class _TextureImpl(_Handle):
+    """CudaBilateralTextureFilter::Impl (src/bilateral_texture_filter_impl.cuh:7-45)."""
+    _destroy = "vip_texture_destroy"
+
+    def __init__(self, width, height, ksize=9, nitr=3, numerics=VIP_NUMERICS_CUDA):
+        super().__init__()
+        self.width, self.height, self.ksize, self.nitr = int(width), int(height), int(ksize), int(nitr)
+        call("vip_texture_create", ctypes.byref(self._h), self.width, self.height, self.ksize, self.nitr,
+             int(numerics))
+
+    def execute(self, d_src, d_dst, stream=None):
+        call("vip_texture_run", self._h, _ptr(d_src), _ptr(d_dst), _stream(stream))
+
+    def compute_blur_and_rtv(self, d_image, d_magnitude, d_blurred, d_rtv, stream=None):
+        call("vip_texture_blur_rtv", self._h, _ptr(d_image), _ptr(d_magnitude), _ptr(d_blurred), _ptr(d_rtv),
+             _stream(stream))
+
+    def compute_guide(self, d_blurred, d_rtv, d_guide, stream=None):
+        call("vip_texture_guide", self._h, _ptr(d_blurred), _ptr(d_rtv), _ptr(d_guide), _stream(stream))
+
+
+class CudaBilateralTextureFilter:
+    """include/cuda/bilateral_texture_filter.hpp:7-17."""
+
+    def __init__(self, width, height, ksize=9, nitr=3, numerics=VIP_NUMERICS_CUDA):
+        self.impl_ = _TextureImpl(width, height, ksize, nitr, numerics)
+
+    def execute(self, d_src, d_dst):
+        self.impl_.execute(d_src, d_dst)
+        device_synchronize()
+
+
+def cuda_gradient(d_src, d_dst, width, height, src_ch=1, numerics=VIP_NUMERICS_CUDA, stream=None):
+    """include/cuda/gradient.hpp:13-23. dtype (uint8 / float32) is taken from a torch
+    tensor; pass ``src_dtype`` via a tensor, raw addresses are treated as uint8.
+    Asynchronous, like src/gradient_impl.cu:90-103."""
+    is_f32 = hasattr(d_src, "dtype") and str(d_src.dtype) == "torch.float32"
+    name = "vip_gradient_f32" if is_f32 else "vip_gradient_u8"
+    call(name, _ptr(d_src), _ptr(d_dst), int(width), int(height), int(src_ch), int(numerics), _stream(stream))
+
+
+class DeviceImage:
+    """include/cuda/device_image.hpp:4-16: dense device buffer, blocking upload/download.
+    ``dtype`` is 'uint8' or 'float32'; host data are numpy arrays (or buffer objects)."""
+
+    _ITEM = {"uint8": 1, "float32": 4}
+
+    def __init__(self, width, height, channels=1, dtype="uint8"):
+        self.nbytes = int(width) * int(height) * int(channels) * self._ITEM[str(dtype)]
+        self._p = ctypes.c_void_p()
+        call("vip_malloc", ctypes.byref(self._p), self.nbytes)
+
+    def get(self) -> int:
+        return self._p.value
+
+    def upload(self, data) -> None:
+        import numpy as np
+        a = np.ascontiguousarray(data)
+        if a.nbytes != self.nbytes:
+            raise ValueError(f"upload of {a.nbytes} bytes into a {self.nbytes}-byte image")
+        call("vip_upload", self._p, a.ctypes.data, self.nbytes)
+
+    def download(self, out) -> None:
+        import numpy as np
+        if not (isinstance(out, np.ndarray) and out.flags.c_contiguous and out.nbytes == self.nbytes):
+            raise ValueError("download target must be a dense numpy array of the image's size")
+        call("vip_download", out.ctypes.data, self._p, self.nbytes)
+
+    def __del__(self):
+        try:
+            if self._p and self._p.value:
+                lib().vip_free(self._p)
+                self._p = ctypes.c_void_p()
+        except Exception:
+            pass

@@ -1,0 +1,111 @@
+"""Row-tile sharding of one frame across GPUs with an r-row halo exchange.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL on ROCm, over
+xGMI). Rank i owns frame rows [row_begin, row_end) in a slab buffer laid out as
+
+    rows [0, r)                 halo above   (received from rank i-1)
+    rows [r, r + n)             own rows
+    rows [r + n, 2r + n)        halo below   (received from rank i+1)
+
+exchange() sends the own top/bottom r rows to the neighbours and receives their
+edge rows into the halos: one sendrecv pair per neighbour, no collective. The
+filter then runs on the slab with neighbour rows clamped to the rows that are
+valid: at the frame's first/last rank the halo is absent and clamping to the
+own rows reproduces the reference's replicate border exactly
+(src/bilateral_filter_impl.cu:50-51), so sharded output == single-GPU output.
+
+The reference has no multi-device code; this is the
+north_star's row-tiled C5 configuration.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+
+def shard_rows(frame_height: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous, balanced row ranges (first ranks take the remainder)."""
+    base, rem = divmod(frame_height, world)
+    begin = rank * base + min(rank, rem)
+    return begin, begin + base + (1 if rank < rem else 0)
+
+
+@dataclass
+class SlabGeometry:
+    width: int
+    frame_height: int
+    radius: int
+    rank: int
+    world: int
+
+    @property
+    def rows(self) -> tuple[int, int]:
+        return shard_rows(self.frame_height, self.world, self.rank)
+
+    @property
+    def own(self) -> int:
+        b, e = self.rows
+        return e - b
+
+    @property
+    def slab_rows(self) -> int:
+        return self.own + 2 * self.radius
+
+    @property
+    def has_above(self) -> bool:
+        return self.rank > 0
+
+    @property
+    def has_below(self) -> bool:
+        return self.rank < self.world - 1
+
+    def clamp_range(self) -> tuple[int, int]:
+        """Slab rows the filter may read (neighbour rows clamp into this range)."""
+        r = self.radius
+        lo = 0 if self.has_above else r
+        hi = self.slab_rows if self.has_below else r + self.own
+        return lo, hi
+
+
+def exchange_halo(slab, geo: SlabGeometry, group=None) -> None:
+    """Fill slab's halo rows from the neighbouring ranks (blocking).
+
+    `slab` is a (slab_rows, width, C) contiguous tensor on this rank's device;
+    for the gloo backend a CPU tensor. Uses batched point-to-point ops so both
+    directions and both neighbours are in flight together.
+    """
+    import torch.distributed as dist
+
+    r, n = geo.radius, geo.own
+    if geo.world == 1 or r == 0:
+        return
+    if n < r:
+        raise ValueError(f"shard of {n} rows is thinner than the halo ({r} rows)")
+    ops = []
+    if geo.has_above:
+        ops.append(dist.P2POp(dist.isend, slab[r:2 * r], geo.rank - 1, group))
+        ops.append(dist.P2POp(dist.irecv, slab[0:r], geo.rank - 1, group))
+    if geo.has_below:
+        ops.append(dist.P2POp(dist.isend, slab[n:n + r], geo.rank + 1, group))
+        ops.append(dist.P2POp(dist.irecv, slab[n + r:n + 2 * r], geo.rank + 1, group))
+    for req in dist.batch_isend_irecv(ops):
+        req.wait()
+
+
+class ShardedBilateral:
+    """Bilateral (or adaptive) filter of a row-sharded frame on the HIP kernels."""
+
+    def __init__(self, width: int, frame_height: int, ksize: int, rank: int, world: int, sigma_space: float = 10.0,
+                 sigma_color: float = 30.0, adaptive: bool = False, numerics: int = 0):
+        from .filters import _AdaptiveImpl, _BilateralImpl
+        self.geo = SlabGeometry(width, frame_height, ksize // 2, rank, world)
+        cls = _AdaptiveImpl if adaptive else _BilateralImpl
+        # the handle's height only sizes nothing on the row-band path; use the slab
+        self.impl = cls(width, self.geo.slab_rows, ksize, sigma_space, sigma_color, numerics)
+        self.adaptive = adaptive
+
+    def filter(self, slab, out, stream=None, exchange: bool = True) -> None:
+        """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3)."""
+        if exchange:
+            exchange_halo(slab, self.geo)
+        lo, hi = self.geo.clamp_range()
+        self.impl.run_rows(slab, out, self.geo.own, self.geo.radius, lo, hi, stream=stream)
