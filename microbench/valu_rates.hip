@@ -1,0 +1,64 @@
+// Microbenchmark: VALU issue rates on gfx950 at 16 waves/CU (4 per SIMD).
+// Each lane runs N iterations of 8 independent chains of one instruction kind.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+#define ITERS 4096
+
+template <int KIND>
+__global__ __launch_bounds__(1024) void k(float* out, float a, float b) {
+    float x[8];
+    for (int i = 0; i < 8; ++i) x[i] = threadIdx.x * 0.001f + i;
+    unsigned u[8];
+    for (int i = 0; i < 8; ++i) u[i] = threadIdx.x * 7919u + i;
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if constexpr (KIND == 0) {
+                asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+            } else if constexpr (KIND == 1) {
+                asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[0]), "v"(*(double*)&x[2]));
+            } else if constexpr (KIND == 2) {
+                asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+            } else if constexpr (KIND == 3) {
+                asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+            } else if constexpr (KIND == 4) {
+                asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(x[i]) : "v"(u[i]));
+            } else if constexpr (KIND == 5) {
+                asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+        }
+    }
+    float s = 0;
+    for (int i = 0; i < 8; ++i) s += x[i] + (float)u[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+template <int KIND>
+double run(const char* name, float* d, int blocks, int pk) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(1024), 0, 0, d, 1.0001f, 0.5f);
+    hipEventRecord(e0);
+    for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k<KIND>, dim3(blocks), dim3(1024), 0, 0, d, 1.0001f, 0.5f);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    double insts = 5.0 * blocks * 16.0 /*waves*/ * ITERS * 8;  // wave-instructions
+    double per_simd_cycles_ns = ms * 1e6 / (insts / (256.0 * 4));  // ns per wave-instr per SIMD
+    printf("%-16s %8.3f ms  %.3f ns per wave-instr per SIMD (= %.2f cycles at 2.4 GHz)%s\n", name, ms / 5, per_simd_cycles_ns,
+           per_simd_cycles_ns * 2.4, pk ? "  [2 f32 per lane]" : "");
+    return ms;
+}
+
+int main() {
+    float* d; hipMalloc(&d, 256 * 1024 * 4 * sizeof(float));
+    int blocks = 256;  // one 1024-thread block per CU
+    run<0>("v_fma_f32", d, blocks, 0);
+    run<1>("v_pk_fma_f32", d, blocks, 1);
+    run<2>("v_sad_u8", d, blocks, 0);
+    run<3>("v_mul_f32", d, blocks, 0);
+    run<4>("v_cvt_f32_ubyte1", d, blocks, 0);
+    run<5>("v_lshl_or_b32", d, blocks, 0);
+    return 0;
+}

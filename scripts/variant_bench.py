@@ -1,0 +1,33 @@
+"""Time bilateral (and adaptive) r=7 on a 4K frame with an alternative libvip build.
+usage: python scripts/variant_bench.py variants/<name>.so [...]  (each in a subprocess)"""
+import json
+import os
+import subprocess
+import sys
+
+CODE = r'''
+import sys, json, torch, ctypes
+sys.path.insert(0, ".")
+import various_image_processings_amd._lib as L
+L.LIB_PATH = sys.argv[1]
+from various_image_processings_amd.filters import _BilateralImpl, _AdaptiveImpl
+torch.cuda.set_device(0)
+W, H = 3840, 2160
+srcs = [torch.randint(0, 255, (H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(6)]
+dst = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
+res = {}
+for name, impl, fn in (("bilateral", _BilateralImpl(W, H, 15), "bilateral_filter"), ("adaptive", _AdaptiveImpl(W, H, 15), "execute")):
+    f = getattr(impl, fn)
+    for i in range(3): f(srcs[i % 6], dst)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    n = 30
+    e0.record()
+    for i in range(n): f(srcs[i % 6], dst)
+    e1.record(); torch.cuda.synchronize()
+    res[name + "_us"] = round(e0.elapsed_time(e1) / n * 1e3, 1)
+print(json.dumps(res))
+'''
+for so in sys.argv[1:]:
+    r = subprocess.run([sys.executable, "-c", CODE, so], capture_output=True, text=True, timeout=300)
+    print(os.path.basename(so), r.stdout.strip() or r.stderr[-500:], flush=True)

@@ -28,124 +28,139 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     constexpr int CB0 = JB / 4, CB1 = (G::L + kP - 1 + R) / 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
-    uint32_t* const plane = lds + lut_words(false);
-
-    const int tile = blockIdx.x;
-    const int tx0 = (tile % a.tiles_x) * kTW;
-    const int ty0 = (tile / a.tiles_x) * TH;
-
-    stage_lut<NT, 1536>(lut, a.color);
-    stage_plane<R, ROWS, NT>(plane, a.src, a.src_pitch, a, tx0, ty0);
-    __syncthreads();
+    uint32_t* const plane = lds + lut_words(true);
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = lane & 15;
-    const int ty = (tid >> 6) * 4 + (lane >> 4);
+    const int ty = wave * 4 + (lane >> 4);
     const uint32_t lane16 = (uint32_t)(lane & 15) << 2;
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
-    // ---- pass 1: box sums over the full square ----
-    uint32_t vrb[NCOL], vg[NCOL], vb[PACK ? 1 : NCOL];
-#pragma unroll
-    for (int j = 0; j < NCOL; ++j) { vrb[j] = 0u; vg[j] = 0u; if constexpr (!PACK) vb[j] = 0u; }
-    for (int r = 0; r < K; ++r) {
-        const uint32_t* row = plane + (ty + r) * G::S + tx * kP;
-        uint32_t px[4 * (CB1 - CB0 + 1)];
-#pragma unroll
-        for (int c = CB0; c <= CB1; ++c) {
-            const uint4 q = *reinterpret_cast<const uint4*>(row + 4 * c);
-            px[4 * (c - CB0) + 0] = q.x; px[4 * (c - CB0) + 1] = q.y;
-            px[4 * (c - CB0) + 2] = q.z; px[4 * (c - CB0) + 3] = q.w;
-        }
-#pragma unroll
-        for (int j = 0; j < NCOL; ++j) {
-            const uint32_t p = px[JB + j - 4 * CB0];
-            if constexpr (PACK) {
-                vrb[j] += p & 0x00ff00ffu;
-                vg[j] += (p >> 8) & 0xffu;
-            } else {
-                vrb[j] += p & 0xffu;
-                vg[j] += (p >> 8) & 0xffu;
-                vb[j] += (p >> 16) & 0xffu;
+    int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x
+    TilePrefetch<R, ROWS, NT> pf;
+    pf.issue(a.src, a.src_pitch, a, (tile % a.tiles_x) * kTW, (tile / a.tiles_x) * TH);
+    stage_lut<NT, 1536>(lut, a.color);
+    pf.commit(plane);
+    __syncthreads();
+
+    while (true) {
+        const int tx0 = (tile % a.tiles_x) * kTW, ty0 = (tile / a.tiles_x) * TH;
+        const int next = tile + (int)gridDim.x;
+        if (next < a.tiles_total) pf.issue(a.src, a.src_pitch, a, (next % a.tiles_x) * kTW, (next / a.tiles_x) * TH);
+        if (ty0 + wave * 4 < a.out_rows) {
+            // ---- pass 1: box sums over the full square ----
+            uint32_t vrb[NCOL], vg[NCOL], vb[PACK ? 1 : NCOL];
+        #pragma unroll
+            for (int j = 0; j < NCOL; ++j) { vrb[j] = 0u; vg[j] = 0u; if constexpr (!PACK) vb[j] = 0u; }
+            for (int r = 0; r < K; ++r) {
+                const uint32_t* row = plane + (ty + r) * G::S + tx * kP;
+                uint32_t px[4 * (CB1 - CB0 + 1)];
+        #pragma unroll
+                for (int c = CB0; c <= CB1; ++c) {
+                    const uint4 q = *reinterpret_cast<const uint4*>(row + 4 * c);
+                    px[4 * (c - CB0) + 0] = q.x; px[4 * (c - CB0) + 1] = q.y;
+                    px[4 * (c - CB0) + 2] = q.z; px[4 * (c - CB0) + 3] = q.w;
+                }
+        #pragma unroll
+                for (int j = 0; j < NCOL; ++j) {
+                    const uint32_t p = px[JB + j - 4 * CB0];
+                    if constexpr (PACK) {
+                        vrb[j] += p & 0x00ff00ffu;
+                        vg[j] += (p >> 8) & 0xffu;
+                    } else {
+                        vrb[j] += p & 0xffu;
+                        vg[j] += (p >> 8) & 0xffu;
+                        vb[j] += (p >> 16) & 0xffu;
+                    }
+                }
             }
-        }
-    }
-    uint32_t ctr[kP];
-    float c0f[kP], c1f[kP], c2f[kP], o0[kP], o1[kP], o2[kP];
-    {
-        const uint32_t* c = plane + (ty + R) * G::S + tx * kP + G::L;
-        const uint4 q0 = *reinterpret_cast<const uint4*>(c);
-        const uint4 q1 = *reinterpret_cast<const uint4*>(c + 4);
-        ctr[0] = q0.x; ctr[1] = q0.y; ctr[2] = q0.z; ctr[3] = q0.w;
-        ctr[4] = q1.x; ctr[5] = q1.y; ctr[6] = q1.z; ctr[7] = q1.w;
-    }
-    {
-        uint32_t wrb = 0u, wg = 0u, wb = 0u;
-#pragma unroll
-        for (int j = 0; j < K; ++j) { wrb += vrb[j]; wg += vg[j]; if constexpr (!PACK) wb += vb[j]; }
-        const float kk = (float)(K * K);
-#pragma unroll
-        for (int i = 0; i < kP; ++i) {
-            if (i > 0) {
-                wrb += vrb[i + K - 1] - vrb[i - 1];
-                wg += vg[i + K - 1] - vg[i - 1];
-                if constexpr (!PACK) wb += vb[i + K - 1] - vb[i - 1];
+            uint32_t ctr[kP];
+            float c0f[kP], c1f[kP], c2f[kP], o0[kP], o1[kP], o2[kP];
+            {
+                const uint32_t* c = plane + (ty + R) * G::S + tx * kP + G::L;
+                const uint4 q0 = *reinterpret_cast<const uint4*>(c);
+                const uint4 q1 = *reinterpret_cast<const uint4*>(c + 4);
+                ctr[0] = q0.x; ctr[1] = q0.y; ctr[2] = q0.z; ctr[3] = q0.w;
+                ctr[4] = q1.x; ctr[5] = q1.y; ctr[6] = q1.z; ctr[7] = q1.w;
             }
-            const uint32_t sr = PACK ? (wrb & 0xffffu) : wrb;
-            const uint32_t sb = PACK ? (wrb >> 16) : wb;
-            c0f[i] = (float)(ctr[i] & 0xffu);
-            c1f[i] = (float)((ctr[i] >> 8) & 0xffu);
-            c2f[i] = (float)((ctr[i] >> 16) & 0xffu);
-            o0[i] = c0f[i] - (float)sr / kk;
-            o1[i] = c1f[i] - (float)wg / kk;
-            o2[i] = c2f[i] - (float)sb / kk;
+            {
+                uint32_t wrb = 0u, wg = 0u, wb = 0u;
+        #pragma unroll
+                for (int j = 0; j < K; ++j) { wrb += vrb[j]; wg += vg[j]; if constexpr (!PACK) wb += vb[j]; }
+                const float kk = (float)(K * K);
+        #pragma unroll
+                for (int i = 0; i < kP; ++i) {
+                    if (i > 0) {
+                        wrb += vrb[i + K - 1] - vrb[i - 1];
+                        wg += vg[i + K - 1] - vg[i - 1];
+                        if constexpr (!PACK) wb += vb[i + K - 1] - vb[i - 1];
+                    }
+                    const uint32_t sr = PACK ? (wrb & 0xffffu) : wrb;
+                    const uint32_t sb = PACK ? (wrb >> 16) : wb;
+                    c0f[i] = (float)(ctr[i] & 0xffu);
+                    c1f[i] = (float)((ctr[i] >> 8) & 0xffu);
+                    c2f[i] = (float)((ctr[i] >> 16) & 0xffu);
+                    o0[i] = c0f[i] - (float)sr / kk;
+                    o1[i] = c1f[i] - (float)wg / kk;
+                    o2[i] = c2f[i] - (float)sb / kk;
+                }
+            }
+
+            // ---- pass 2: offset-weighted bilateral over the disc ----
+            float s0[kP], s1[kP], s2[kP], sk[kP];
+        #pragma unroll
+            for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
+
+            for (int ky = -R; ky <= R; ++ky) {
+                const int aky = ky < 0 ? -ky : ky;
+                const int hw = circle_hw(R, aky);
+                set_progress_priority((ky + R) * 4 / (2 * R + 1));
+                const int row_off = (ty + R + ky) * G::S + tx * kP;
+                const float* const ws = a.ws + aky * kWsStride;
+                HwDispatch<R, 0>::run(hw, [&](auto hwc) {
+                    constexpr int HW = decltype(hwc)::value;
+                    constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
+                    constexpr int NC = C1 - C0 + 1;
+                    uint32_t gp[4 * NC];
+                    load_row<C0, NC>(plane, row_off, gp);
+                    float wsv[HW + 1];
+        #pragma unroll
+                    for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
+                    // dist = |(n0-c0)-o0| + |(n1-c1)-o1| + |(n2-c2)-o2|; (float)(n-c) == f_n - f_c exactly.
+                    // Index int(dist) <= 1530 -> word d*16 + (lane & 15) of the 1536 x 16 LUT.
+                    auto widx = [&](uint32_t, float f0, float f1, float f2, int i) {
+                        const float d0 = (f0 - c0f[i]) - o0[i];
+                        const float d1 = (f1 - c1f[i]) - o1[i];
+                        const float d2 = (f2 - c2f[i]) - o2[i];
+                        const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
+                        return ((uint32_t)dist << 6) | lane16;
+                    };
+                    row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, gp, wsv, lut_bytes, widx, s0, s1, s2, sk);
+                });
+            }
+
+            uint32_t o[kP];
+        #pragma unroll
+            for (int i = 0; i < kP; ++i) {
+                o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) | (f2u8(s2[i] / sk[i] + 0.5f) << 16);
+            }
+            store8(a, ty0 + ty, tx0 + tx * kP, o);
         }
+        if (next >= a.tiles_total) break;
+        __syncthreads();
+        pf.commit(plane);
+        __syncthreads();
+        tile = next;
     }
-
-    // ---- pass 2: offset-weighted bilateral over the disc ----
-    float s0[kP], s1[kP], s2[kP], sk[kP];
-#pragma unroll
-    for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
-
-    for (int ky = -R; ky <= R; ++ky) {
-        const int aky = ky < 0 ? -ky : ky;
-        const int hw = circle_hw(R, aky);
-        const int row_off = (ty + R + ky) * G::S + tx * kP;
-        const float* const ws = a.ws + aky * kWsStride;
-        HwDispatch<R, 0>::run(hw, [&](auto hwc) {
-            constexpr int HW = decltype(hwc)::value;
-            constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
-            constexpr int NC = C1 - C0 + 1;
-            uint32_t gp[4 * NC];
-            load_row<C0, NC>(plane, row_off, gp);
-            float wsv[HW + 1];
-#pragma unroll
-            for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
-            // dist = |(n0-c0)-o0| + |(n1-c1)-o1| + |(n2-c2)-o2|; (float)(n-c) == f_n - f_c exactly.
-            // Index int(dist) <= 1530 -> word d*16 + (lane & 15) of the 1536 x 16 LUT.
-            auto widx = [&](uint32_t, float f0, float f1, float f2, int i) {
-                const float d0 = (f0 - c0f[i]) - o0[i];
-                const float d1 = (f1 - c1f[i]) - o1[i];
-                const float d2 = (f2 - c2f[i]) - o2[i];
-                const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
-                return ((uint32_t)dist << 6) | lane16;
-            };
-            row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, gp, wsv, lut_bytes, widx, s0, s1, s2, sk);
-        });
-    }
-
-    uint32_t o[kP];
-#pragma unroll
-    for (int i = 0; i < kP; ++i) {
-        o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) | (f2u8(s2[i] / sk[i] + 0.5f) << 16);
-    }
-    store8(a, ty0 + ty, tx0 + tx * kP, o);
 }
 
 template <int R, bool FMA>
 static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
-    constexpr int WAVES = pick_waves<R, 1>();
+    // 8 waves: the per-output centre/offset floats (48 VGPRs) plus the pipelined
+    // LUT reads need more than the 128 VGPRs a 16-wave workgroup allows
+    constexpr int WAVES = pick_waves<R, 1, 8>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
     constexpr int LDS = lds_bytes<R, WAVES, 1>();
@@ -156,10 +171,11 @@ static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
         attr_done = true;
     }
-    const int tiles_y = (a.out_rows + TH - 1) / TH;
-    const int blocks = a.tiles_x * tiles_y;
-    if (blocks == 0) return 0;
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, a);
+    StencilArgs args = a;
+    args.tiles_total = a.tiles_x * ((a.out_rows + TH - 1) / TH);
+    if (args.tiles_total == 0) return 0;
+    const int blocks = persistent_blocks(args.tiles_total);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }
 

@@ -18,6 +18,18 @@
 
 namespace vip {
 
+#ifdef VIP_STAMPS
+// diagnostic build only: [block][wave][tile][3] shader-clock stamps
+__device__ unsigned long long vip_stamps[256 * 16 * 8 * 3];
+__device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
+    if ((threadIdx.x & 63) == 0 && t < 8 && blk < 256)
+        vip_stamps[((blk * 16 + wave) * 8 + t) * 3 + k] = __builtin_amdgcn_s_memtime();
+}
+#define VIP_STAMP(t, k) vip_stamp(blockIdx.x, wave, t, k)
+#else
+#define VIP_STAMP(t, k)
+#endif
+
 template <int R, int WAVES, bool JOINT, bool FMA>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R>;
@@ -30,69 +42,95 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     uint32_t* const gplane = lds + lut_words(false);
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
-    const int tile = blockIdx.x;
-    const int tx0 = (tile % a.tiles_x) * kTW;
-    const int ty0 = (tile / a.tiles_x) * TH;
-
-    stage_lut<NT, 768>(lut, a.color);
-    stage_plane<R, ROWS, NT>(gplane, a.guide, a.guide_pitch, a, tx0, ty0);
-    if constexpr (JOINT) stage_plane<R, ROWS, NT>(splane, a.src, a.src_pitch, a, tx0, ty0);
-    __syncthreads();
-
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = lane & 15;
-    const int ty = (tid >> 6) * 4 + (lane >> 4);
+    const int ty = wave * 4 + (lane >> 4);
     const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
-    // centre pixels of the guide (== src for the plain filter)
-    uint32_t ctr[kP];
+    // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
+    int tile = blockIdx.x;
+    TilePrefetch<R, ROWS, NT> pg, ps;
     {
-        const uint32_t* c = gplane + (ty + R) * G::S + tx * kP + G::L;
-        const uint4 c0 = *reinterpret_cast<const uint4*>(c);
-        const uint4 c1 = *reinterpret_cast<const uint4*>(c + 4);
-        ctr[0] = c0.x; ctr[1] = c0.y; ctr[2] = c0.z; ctr[3] = c0.w;
-        ctr[4] = c1.x; ctr[5] = c1.y; ctr[6] = c1.z; ctr[7] = c1.w;
+        const int tx0 = (tile % a.tiles_x) * kTW, ty0 = (tile / a.tiles_x) * TH;
+        pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
+        if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
-    float s0[kP], s1[kP], s2[kP], sk[kP];
-#pragma unroll
-    for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
+    stage_lut<NT, 768>(lut, a.color);  // once per workgroup
+    pg.commit(gplane);
+    if constexpr (JOINT) ps.commit(splane);
+    __syncthreads();
 
-    for (int ky = -R; ky <= R; ++ky) {
-        const int aky = ky < 0 ? -ky : ky;
-        const int hw = circle_hw(R, aky);
-        const int row_off = (ty + R + ky) * G::S + tx * kP;
-        const float* const ws = a.ws + aky * kWsStride;
-        HwDispatch<R, 0>::run(hw, [&](auto hwc) {
-            constexpr int HW = decltype(hwc)::value;
-            constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
-            constexpr int NC = C1 - C0 + 1;
-            uint32_t gp[4 * NC];
-            uint32_t sp[4 * NC];
-            load_row<C0, NC>(gplane, row_off, gp);
-            if constexpr (JOINT) load_row<C0, NC>(splane, row_off, sp);
-            else {
-#pragma unroll
-                for (int q = 0; q < 4 * NC; ++q) sp[q] = gp[q];
+    for (int it = 0;; ++it) {
+        VIP_STAMP(it, 0);
+        const int tx0 = (tile % a.tiles_x) * kTW, ty0 = (tile / a.tiles_x) * TH;
+        const int next = tile + (int)gridDim.x;
+        if (next < a.tiles_total) {  // next tile's HBM reads fly under this tile's taps
+            const int nx0 = (next % a.tiles_x) * kTW, ny0 = (next / a.tiles_x) * TH;
+            pg.issue(a.guide, a.guide_pitch, a, nx0, ny0);
+            if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
+        }
+        if (ty0 + wave * 4 < a.out_rows) {  // wave-uniform: skip rows past the frame
+            uint32_t ctr[kP];  // centre pixels of the guide (== src for the plain filter)
+            {
+                const uint4* c = reinterpret_cast<const uint4*>(gplane + (ty + R) * G::S + tx * kP + G::L);
+                const uint4 c0 = c[0], c1 = c[1];
+                ctr[0] = c0.x; ctr[1] = c0.y; ctr[2] = c0.z; ctr[3] = c0.w;
+                ctr[4] = c1.x; ctr[5] = c1.y; ctr[6] = c1.z; ctr[7] = c1.w;
             }
-            float wsv[HW + 1];
+            float s0[kP], s1[kP], s2[kP], sk[kP];
 #pragma unroll
-            for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
-            // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*32 + (lane & 31)
-            auto widx = [&](uint32_t g, float, float, float, int i) {
-                return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << 7) | lane4;
-            };
-            row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, sp, wsv, lut_bytes, widx, s0, s1, s2, sk);
-        });
-    }
+            for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
 
-    uint32_t o[kP];
+            for (int ky = -R; ky <= R; ++ky) {
+                const int aky = ky < 0 ? -ky : ky;
+                const int hw = circle_hw(R, aky);
+                set_progress_priority((ky + R) * 4 / (2 * R + 1));
+                const int row_off = (ty + R + ky) * G::S + tx * kP;
+                const float* const ws = a.ws + aky * kWsStride;
+                HwDispatch<R, 0>::run(hw, [&](auto hwc) {
+                    constexpr int HW = decltype(hwc)::value;
+                    constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
+                    constexpr int NC = C1 - C0 + 1;
+                    uint32_t gp[4 * NC];
+                    uint32_t sp[4 * NC];
+                    load_row<C0, NC>(gplane, row_off, gp);
+                    if constexpr (JOINT) {
+                        load_row<C0, NC>(splane, row_off, sp);
+                    } else {
 #pragma unroll
-    for (int i = 0; i < kP; ++i) {
-        o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) | (f2u8(s2[i] / sk[i] + 0.5f) << 16);
+                        for (int q = 0; q < 4 * NC; ++q) sp[q] = gp[q];
+                    }
+                    float wsv[HW + 1];
+#pragma unroll
+                    for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
+                    // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*32 + (lane & 31)
+                    auto widx = [&](uint32_t g, float, float, float, int i) {
+                        return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << 7) | lane4;
+                    };
+                    row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, sp, wsv, lut_bytes, widx, s0, s1, s2, sk);
+                });
+            }
+
+            uint32_t o[kP];
+#pragma unroll
+            for (int i = 0; i < kP; ++i) {
+                o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) |
+                       (f2u8(s2[i] / sk[i] + 0.5f) << 16);
+            }
+            store8(a, ty0 + ty, tx0 + tx * kP, o);
+        }
+        VIP_STAMP(it, 1);
+        if (next >= a.tiles_total) break;
+        __syncthreads();  // every wave is done reading this tile
+        pg.commit(gplane);
+        if constexpr (JOINT) ps.commit(splane);
+        __syncthreads();
+        VIP_STAMP(it, 2);
+        tile = next;
     }
-    store8(a, ty0 + ty, tx0 + tx * kP, o);
 }
 
 template <int R, bool JOINT, bool FMA>
@@ -109,10 +147,11 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
         attr_done = true;
     }
-    const int tiles_y = (a.out_rows + TH - 1) / TH;
-    const int blocks = a.tiles_x * tiles_y;
-    if (blocks == 0) return 0;
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, a);
+    StencilArgs args = a;
+    args.tiles_total = a.tiles_x * ((a.out_rows + TH - 1) / TH);
+    if (args.tiles_total == 0) return 0;
+    const int blocks = persistent_blocks(args.tiles_total);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }
 
@@ -145,6 +184,13 @@ int launch_bilateral_joint_mul(int radius, const StencilArgs& a, hipStream_t s) 
 int launch_bilateral_plain_fma(int radius, const StencilArgs& a, hipStream_t s) {
     return launch_bilateral_dispatch<false, true>(radius, a, s);
 }
+#ifdef VIP_STAMPS
+}  // namespace vip
+extern "C" int vip_debug_read_stamps(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vip::vip_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+namespace vip {
+#endif
 #else
 int launch_bilateral_plain_mul(int radius, const StencilArgs& a, hipStream_t s) {
     return launch_bilateral_dispatch<false, false>(radius, a, s);

@@ -33,11 +33,25 @@ struct StencilArgs {
     int src_row0;          // source row of output row 0
     int row_lo, row_hi;    // neighbour rows clamp to [row_lo, row_hi)
     int tiles_x;
+    int tiles_total;       // tiles_x * tiles_y (persistent workgroups stride over them)
     int aligned;           // src/guide base and pitch are 4-byte aligned -> dword tile loads
     int dst_aligned;       // dst base and pitch are 8-byte aligned -> qword stores
     const float* color;    // colour LUT in device memory
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
+
+// One workgroup per CU (the 96 KiB LUT fills most of the CU's LDS), each striding
+// over tiles; fewer blocks than CUs when the frame has fewer tiles.
+inline int persistent_blocks(int tiles) {
+    static int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        return n;
+    }();
+    return tiles < cus ? tiles : cus;
+}
 
 constexpr int lut_words(bool adaptive) { return adaptive ? 1536 * 16 : 768 * 32; }
 
@@ -48,10 +62,10 @@ struct Geom {
     static constexpr int GROUPS = (kTW + 2 * L) / 4;        // 4-pixel groups per tile row
 };
 
-// Largest wave count (16, 8 or 4) whose LUT + plane(s) fit the CU's LDS.
-template <int R, int PLANES>
+// Largest wave count (<= MAXW: 16, 8 or 4) whose LUT + plane(s) fit the CU's LDS.
+template <int R, int PLANES, int MAXW = 16>
 constexpr int pick_waves() {
-    for (int w = 16; w >= 4; w /= 2) {
+    for (int w = MAXW; w >= 4; w /= 2) {
         const long long bytes = 4LL * lut_words(false) + 4LL * PLANES * (w * 4 + 2 * R) * Geom<R>::S;
         if (bytes <= kLdsBudget) return w;
     }
@@ -96,32 +110,60 @@ __device__ __forceinline__ uint32_t load_rgb(const uint8_t* row, int x) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
 }
 
-// Stage source rows [ty0 + src_row0 - R, ... + ROWS) x columns [tx0 - L, tx0 - L + TW + 2L)
-// of `img` into `plane`, clamping rows to [row_lo, row_hi) and columns to [0, width).
+// Register-staged prefetch of one tile plane: source rows
+// [ty0 + src_row0 - R, +ROWS) x columns [tx0 - L, tx0 - L + TW + 2L) of `img`, rows
+// clamped to [row_lo, row_hi), columns to [0, width) (the reference's replicate
+// border, src/bilateral_filter_impl.cu:47-56). issue() starts the global loads
+// (3 dwords per 4-pixel group when the group is interior and dword aligned,
+// byte loads otherwise) and returns at once; commit() unpacks RGB to RGBX words
+// and writes the LDS plane. A persistent workgroup issues tile t+1 before it
+// computes tile t, so HBM latency hides under the VALU-bound tap loop.
 template <int R, int ROWS, int NT>
-__device__ __forceinline__ void stage_plane(uint32_t* plane, const uint8_t* img, long long pitch, const StencilArgs& a,
-                                            int tx0, int ty0) {
+struct TilePrefetch {
     using G = Geom<R>;
-    const int tid = threadIdx.x;
-    for (int g = tid; g < ROWS * G::GROUPS; g += NT) {
-        const int r = g / G::GROUPS;
-        const int gc = g - r * G::GROUPS;
-        const int sy = clampi(ty0 + a.src_row0 - R + r, a.row_lo, a.row_hi - 1);
-        const uint8_t* row = img + (long long)sy * pitch;
-        const int x = tx0 - G::L + 4 * gc;
-        uint4 q;
-        if (a.aligned && x >= 0 && x + 3 < a.width) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
-            q = unpack_rgb4(w[0], w[1], w[2]);
-        } else {
-            q.x = load_rgb(row, clampi(x + 0, 0, a.width - 1));
-            q.y = load_rgb(row, clampi(x + 1, 0, a.width - 1));
-            q.z = load_rgb(row, clampi(x + 2, 0, a.width - 1));
-            q.w = load_rgb(row, clampi(x + 3, 0, a.width - 1));
+    static constexpr int NG = ROWS * G::GROUPS;
+    static constexpr int K = (NG + NT - 1) / NT;
+    uint32_t raw[K][3];
+
+    __device__ __forceinline__ void issue(const uint8_t* img, long long pitch, const StencilArgs& a, int tx0,
+                                          int ty0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int g = (int)threadIdx.x + k * NT;
+            if (NG % NT != 0 && k == K - 1 && g >= NG) continue;
+            const int r = g / G::GROUPS;
+            const int gc = g - r * G::GROUPS;
+            const int sy = clampi(ty0 + a.src_row0 - R + r, a.row_lo, a.row_hi - 1);
+            const uint8_t* row = img + (long long)sy * pitch;
+            const int x = tx0 - G::L + 4 * gc;
+            if (a.aligned && x >= 0 && x + 3 < a.width) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
+                raw[k][0] = w[0];
+                raw[k][1] = w[1];
+                raw[k][2] = w[2];
+            } else {
+                const uint32_t q0 = load_rgb(row, clampi(x + 0, 0, a.width - 1));
+                const uint32_t q1 = load_rgb(row, clampi(x + 1, 0, a.width - 1));
+                const uint32_t q2 = load_rgb(row, clampi(x + 2, 0, a.width - 1));
+                const uint32_t q3 = load_rgb(row, clampi(x + 3, 0, a.width - 1));
+                raw[k][0] = q0 | (q1 << 24);
+                raw[k][1] = (q1 >> 8) | (q2 << 16);
+                raw[k][2] = (q2 >> 16) | (q3 << 8);
+            }
         }
-        *reinterpret_cast<uint4*>(plane + r * G::S + 4 * gc) = q;
     }
-}
+
+    __device__ __forceinline__ void commit(uint32_t* plane) const {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int g = (int)threadIdx.x + k * NT;
+            if (NG % NT != 0 && k == K - 1 && g >= NG) continue;
+            const int r = g / G::GROUPS;
+            const int gc = g - r * G::GROUPS;
+            *reinterpret_cast<uint4*>(plane + r * G::S + 4 * gc) = unpack_rgb4(raw[k][0], raw[k][1], raw[k][2]);
+        }
+    }
+};
 
 // Fill the interleaved colour LUT: word d*COPIES + c = color[d], for
 // 768 entries x 32 copies (bilateral) or 1536 x 16 (adaptive) = 96 KiB.
@@ -139,32 +181,65 @@ __device__ __forceinline__ void stage_lut(uint32_t* lut, const float* color) {
 // (row_off is 16-byte aligned; indexing as uint4 lets hipcc emit ds_read_b128).
 template <int C0, int NC>
 __device__ __forceinline__ void load_row(const uint32_t* plane, int row_off, uint32_t (&w)[4 * NC]) {
-    const uint4* v = reinterpret_cast<const uint4*>(plane) + (row_off >> 2) + C0;
+    // volatile: keep every load a full ds_read_b128 (hipcc otherwise narrows the
+    // edge chunks to the words the row uses and re-pairs them as misaligned,
+    // bank-conflicting ds_read2_b32)
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(3))) const volatile u32x4 lds_u32x4;
+    lds_u32x4* v = (lds_u32x4*)(plane) + (row_off >> 2) + C0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
-        const uint4 q = v[c];
+        const u32x4 q = v[c];
         w[4 * c + 0] = q.x; w[4 * c + 1] = q.y; w[4 * c + 2] = q.z; w[4 * c + 3] = q.w;
     }
 }
 
+// Progress-based wave priority. The SIMD arbiter serves ready waves by priority,
+// then age, so with equal priorities the oldest wave of each SIMD races through
+// the tile and idles at the tile barrier while the youngest finishes alone
+// (measured with s_memtime stamps: 67K vs 116K cycles for the same work).
+// Lowering a wave's priority as it advances through the tile's rows hands the
+// issue slots to the waves that are behind, so all reach the barrier together.
+// `band` is 0..3 (first quarter of the rows .. last quarter).
+__device__ __forceinline__ void set_progress_priority(int band) {
+#ifndef VIP_NO_PRIO_BANDS
+    switch (band) {  // s_setprio takes an immediate; band is wave-uniform
+        case 0: __builtin_amdgcn_s_setprio(3); break;
+        case 1: __builtin_amdgcn_s_setprio(2); break;
+        case 2: __builtin_amdgcn_s_setprio(1); break;
+        default: __builtin_amdgcn_s_setprio(0); break;
+    }
+#else
+    (void)band;
+#endif
+}
+
+// LUT-read lookahead of the tap loop, in neighbour columns (build knob).
+#ifndef VIP_PIPE_DEPTH
+#define VIP_PIPE_DEPTH 1
+#endif
+
 // The tap loop of one tile row for the thread's kP outputs, software-pipelined
-// one neighbour column ahead: while column j's weights are accumulated, column
-// j+1's colour-LUT reads are already in flight (the LDS latency is hidden inside
-// the wave instead of only across waves). `widx(g, f0, f1, f2, i)` returns the LDS
-// byte address of the colour weight of guide word g (source floats f*) for output i.
-// Accumulation order per output is ascending kx, as in the reference's row-major loop.
+// VIP_PIPE_DEPTH neighbour columns ahead: while column j's weights are
+// accumulated, the colour-LUT reads of columns j+1..j+D are already in flight
+// (the LDS latency is hidden inside the wave, not only across waves).
+// `widx(g, f0, f1, f2, i)` returns the LDS byte address of the colour weight of
+// guide word g (source floats f*) for output i. Accumulation order per output is
+// ascending kx, as in the reference's row-major loop.
 template <int HW, int L, int C0, int NGP, bool FMA, class WIdx>
 __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32_t (&sp)[NGP],
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
                                          float (&s0)[kP], float (&s1)[kP], float (&s2)[kP], float (&sk)[kP]) {
+    constexpr int D = VIP_PIPE_DEPTH;
+    constexpr int NB = D + 1;            // ring of in-flight columns
     constexpr int J0 = L - HW;           // first neighbour column relative to the thread's 8
     constexpr int J1 = L + kP - 1 + HW;  // last
-    float wc[2][kP];
-    float nf[2][3];
+    float wc[NB][kP];
+    float nf[NB][3];
     auto issue = [&](int j) {
         const uint32_t g = gp[j - 4 * C0];
         const uint32_t p = sp[j - 4 * C0];
-        float* f = nf[j & 1];
+        float* f = nf[(j - J0) % NB];
         f[0] = (float)(p & 0xffu);
         f[1] = (float)((p >> 8) & 0xffu);
         f[2] = (float)((p >> 16) & 0xffu);
@@ -172,19 +247,20 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
         for (int i = 0; i < kP; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            wc[j & 1][i] = *reinterpret_cast<const float*>(lut + widx(g, f[0], f[1], f[2], i));
+            wc[(j - J0) % NB][i] = *reinterpret_cast<const float*>(lut + widx(g, f[0], f[1], f[2], i));
         }
     };
-    issue(J0);
+#pragma unroll
+    for (int j = J0; j < J0 + D && j <= J1; ++j) issue(j);
 #pragma unroll
     for (int j = J0; j <= J1; ++j) {
-        if (j < J1) issue(j + 1);
-        const float* f = nf[j & 1];
+        if (j + D <= J1) issue(j + D);
+        const float* f = nf[(j - J0) % NB];
 #pragma unroll
         for (int i = 0; i < kP; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            const float w = wc[j & 1][i] * wsv[kx < 0 ? -kx : kx];
+            const float w = wc[(j - J0) % NB][i] * wsv[kx < 0 ? -kx : kx];
             if constexpr (FMA) {
                 s0[i] = __builtin_fmaf(f[0], w, s0[i]);
                 s1[i] = __builtin_fmaf(f[1], w, s1[i]);
@@ -196,7 +272,9 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
             }
             sk[i] = sk[i] + w;
         }
+#ifndef VIP_NO_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
