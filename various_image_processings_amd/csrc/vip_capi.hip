@@ -34,6 +34,8 @@ int launch_blur_rtv(const uint8_t* img, const float* mag, float* blurred, float*
                     int ksize, bool cpp, hipStream_t stream);
 int launch_guide(const float* blurred, const float* rtv, uint8_t* guide, int width, int height, int ksize, bool cpp,
                  hipStream_t stream);
+int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, bool cpp,
+                               hipStream_t stream);
 
 // LUT construction. CUDA profile: src/bilateral_filter_impl.cu:217-237 (float
 // coefficient, std::exp(float) == expf). CPP profile: include/cpp/bilateral_filter.hpp:13-36
@@ -322,6 +324,7 @@ int vip_texture_guide(vip_texture_t h, const float* d_blurred, const float* d_rt
 // Impl::execute (src/bilateral_texture_filter_impl.cu:199-214) without the
 // nitr + 2 device-to-device copies: iteration i reads X_i and writes X_{i+1},
 // X_0 = d_src, X_nitr = d_dst, intermediates alternate between two scratch frames.
+// Each iteration is two launches: the fused guide stage and the joint bilateral.
 int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream) {
     if (!h || !d_src || !d_dst) return VIP_ERR_INVALID_ARGUMENT;
     const hipStream_t s = (hipStream_t)stream;
@@ -338,9 +341,9 @@ int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void*
     }
     for (int it = 0; it < h->nitr; ++it) {
         uint8_t* next = (it == h->nitr - 1) ? d_dst : (cur == h->d_ping[0] ? h->d_ping[1] : h->d_ping[0]);
-        int rc = launch_gradient_u8(cur, h->d_mag, h->width, h->height, 3, s);
-        if (!rc) rc = vip_texture_blur_rtv(h, cur, h->d_mag, h->d_blurred, h->d_rtv, stream);
-        if (!rc) rc = vip_texture_guide(h, h->d_blurred, h->d_rtv, h->d_guide, stream);
+        // gradient -> blur/mRTV -> guide fused in LDS (one launch), then the JBF
+        int rc = launch_texture_guide_fused(cur, h->d_guide, h->width, h->height, h->ksize,
+                                            h->numerics == VIP_NUMERICS_CPP, s);
         if (!rc) rc = vip_joint_bilateral_run(h->jbf, cur, pitch, h->d_guide, pitch, next, pitch, stream);
         if (rc) return rc;
         cur = next;

@@ -112,30 +112,33 @@ __global__ __launch_bounds__(256) void blur_rtv_kernel(const uint8_t* __restrict
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int x = x0 + tx, y = y0 + ty;
     if (x >= width || y >= height) return;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    float imax = 0.f, imin = 256.f, mmax = 0.f, msum = 0.f;
+    // channel sums are exact integers (== the reference's float sums, all < 2^24);
+    // intensity extremes come from integer byte sums: x -> float(x)/3.f is monotonic,
+    // so max_i(s_i/3.f) == (max_i s_i)/3.f and one divide replaces k*k of them
+    uint32_t s0 = 0, s1 = 0, s2 = 0, smax = 0, smin = 0xffffffffu;
+    float mmax = 0.f, msum = 0.f;
     for (int ky = 0; ky < ksize; ++ky) {
         const uint32_t* ri = s_img + (ty + ky) * tw + tx;
         const float* rm = s_mag + (ty + ky) * tw + tx;
         for (int kx = 0; kx < ksize; ++kx) {
             const uint32_t p = ri[kx];
-            const uint32_t b0 = p & 0xffu, b1 = (p >> 8) & 0xffu, b2 = (p >> 16) & 0xffu;
-            s0 = s0 + (float)b0;
-            s1 = s1 + (float)b1;
-            s2 = s2 + (float)b2;
-            const float inten = (float)(int)(b0 + b1 + b2) / 3.f;
-            imax = imax < inten ? inten : imax;
-            imin = inten < imin ? inten : imin;
+            s0 += p & 0xffu;
+            s1 += (p >> 8) & 0xffu;
+            s2 += (p >> 16) & 0xffu;
+            const uint32_t s = __builtin_amdgcn_sad_u8(p, 0u, 0u);
+            smax = s > smax ? s : smax;
+            smin = s < smin ? s : smin;
             const float m = rm[kx];
             mmax = mmax < m ? m : mmax;
-            msum = msum + m;
+            msum = msum + m;  // row-major order, as the reference accumulates
         }
     }
     const float kk = (float)(ksize * ksize);
     float* b = blurred + ((long long)y * width + x) * 3;
-    b[0] = s0 / kk;
-    b[1] = s1 / kk;
-    b[2] = s2 / kk;
+    b[0] = (float)s0 / kk;
+    b[1] = (float)s1 / kk;
+    b[2] = (float)s2 / kk;
+    const float imax = (float)(int)smax / 3.f, imin = (float)(int)smin / 3.f;
     const float num = (imax - imin) * mmax;
     rtv[(long long)y * width + x] = CPP ? num / (msum + 1e-9f) : (float)((double)num / ((double)msum + 1e-9));
 }
@@ -216,6 +219,268 @@ int launch_guide(const float* blurred, const float* rtv, uint8_t* guide, int wid
     else
         hipLaunchKernelGGL(guide_kernel<false>, grid, dim3(256), lds, stream, blurred, rtv, guide, width, height, ksize);
     return (int)hipGetLastError();
+}
+
+}  // namespace vip
+
+namespace vip {
+
+// ---------------------------------------------------------------------------
+// Fused guide stage of one bilateral-texture iteration: X (u8x3) -> G (u8x3).
+// gradient (src/gradient_impl.cu:7-66) -> box blur + mRTV
+// (src/bilateral_texture_filter_impl.cu:10-104) -> argmin/alpha blend (:106-177),
+// all in LDS: blurred and rtv never reach HBM (reads 3 B/px + halo, writes 3 B/px).
+//
+// Regions around the output tile T (64 x 16), R = ksize/2, each stored
+// PRE-CLAMPED: entry q holds the stage's value at clamp(q), which is exactly what
+// the reference stage reads through its own clamped coordinates. Inner loops then
+// index the regions directly; a position outside the image only clamps its
+// centre once.
+//   XR : T (+) (2R+1)  image pixels as RGBX words (origin 4-px aligned)
+//   MR : T (+) 2R      gradient magnitude
+//   BR, RR : T (+) R   blurred RGB and rtv
+// Bit-exact with the stage kernels: integer box sums (exact), intensity extremes
+// from integer byte sums (x/3.f is monotonic), magnitude sum accumulated in the
+// reference's row-major order, rtv divide in double (CUDA profile).
+// ---------------------------------------------------------------------------
+constexpr int kGfTW = 64, kGfTH = 16, kGfNT = 256, kGfRun = 4;
+
+template <int R>
+struct GfGeom {
+    static constexpr int XL = round_up(2 * R + 1, 4);          // XR left apron (aligned)
+    // widths padded so the runs of kGfRun positions that overhang the real
+    // regions (their results are never read) stay inside their source rows
+    static constexpr int XW = round_up(kGfTW + XL + 2 * R + 1 + 8, 4);
+    static constexpr int XH = kGfTH + 4 * R + 2;
+    static constexpr int MW = round_up(kGfTW + 4 * R + 4, kGfRun);
+    static constexpr int MH = kGfTH + 4 * R;
+    static constexpr int BW = round_up(kGfTW + 2 * R, kGfRun);
+    static constexpr int BH = kGfTH + 2 * R;
+    static constexpr int WORDS = XW * XH + MW * MH + 4 * BW * BH;
+};
+
+template <int R, bool CPP>
+__global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
+                                                                   uint8_t* __restrict__ guide, int width,
+                                                                   int height, int aligned) {
+    using G = GfGeom<R>;
+    constexpr int K = 2 * R + 1;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* XR = lds;
+    float* MR = reinterpret_cast<float*>(XR + G::XW * G::XH);
+    float* BR = MR + G::MW * G::MH;  // 3 planes of BW*BH
+    float* RR = BR + 3 * G::BW * G::BH;
+    const int x0 = blockIdx.x * kGfTW, y0 = blockIdx.y * kGfTH;
+    const int tid = threadIdx.x;
+    // region origins (image coordinates)
+    const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
+    const int mr0x = x0 - 2 * R, mr0y = y0 - 2 * R;
+    const int br0x = x0 - R, br0y = y0 - R;
+    const int W1 = width - 1, H1 = height - 1;
+
+    // 1. XR: 4-pixel groups, dword loads when interior and aligned, clamped bytes otherwise
+    for (int g = tid; g < G::XH * (G::XW / 4); g += kGfNT) {
+        const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
+        const uint8_t* row = img + (long long)clampi(yr0 + ry, 0, H1) * width * 3;
+        const int x = xr0 + 4 * gx;
+        uint4 q;
+        if (aligned && x >= 0 && x + 3 <= W1) {
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
+            q = unpack_rgb4(w[0], w[1], w[2]);
+        } else {
+            q.x = load_rgb(row, clampi(x, 0, W1));
+            q.y = load_rgb(row, clampi(x + 1, 0, W1));
+            q.z = load_rgb(row, clampi(x + 2, 0, W1));
+            q.w = load_rgb(row, clampi(x + 3, 0, W1));
+        }
+        *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = q;
+    }
+    __syncthreads();
+
+    // 2. MR[q] = gradient at c = clamp(q); XR is pre-clamped, so c's neighbours
+    //    are read directly (XR[c +- e] == X(clamp(c +- e)))
+    for (int i = tid; i < G::MW * G::MH; i += kGfNT) {
+        const int qy = i / G::MW, qx = i - qy * G::MW;
+        const int cx = clampi(mr0x + qx, 0, W1) - xr0, cy = clampi(mr0y + qy, 0, H1) - yr0;
+        const uint32_t* c = XR + cy * G::XW + cx;
+        const uint32_t L = c[-1], Rt = c[1], U = c[-G::XW], D = c[G::XW];
+        float dx = 0.f, dy = 0.f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) {
+            const int h = (int)((Rt >> (8 * ch)) & 0xffu) - (int)((L >> (8 * ch)) & 0xffu);
+            const int v = (int)((D >> (8 * ch)) & 0xffu) - (int)((U >> (8 * ch)) & 0xffu);
+            dx = dx + (float)(h * h);
+            dy = dy + (float)(v * v);
+        }
+        MR[i] = __builtin_sqrtf(dx + dy);
+    }
+    __syncthreads();
+
+    // 3. box blur + mRTV, kGfRun horizontally adjacent positions per thread
+    const float kk = (float)(K * K);
+    for (int run = tid; run < G::BH * (G::BW / kGfRun); run += kGfNT) {
+        const int py = run / (G::BW / kGfRun), px0 = (run - py * (G::BW / kGfRun)) * kGfRun;
+        const int iy = br0y + py, ix0 = br0x + px0;
+        uint32_t s0[kGfRun], s1[kGfRun], s2[kGfRun], smax[kGfRun], smin[kGfRun];
+        float mmax[kGfRun], msum[kGfRun];
+#pragma unroll
+        for (int j = 0; j < kGfRun; ++j) {
+            s0[j] = s1[j] = s2[j] = smax[j] = 0u;
+            smin[j] = 0xffffffffu;
+            mmax[j] = msum[j] = 0.f;
+        }
+        if (iy >= 0 && iy <= H1 && ix0 >= 0 && ix0 + kGfRun - 1 <= W1) {
+            // all centres inside the image: shared row segments
+            for (int ky = -R; ky <= R; ++ky) {
+                const uint32_t* xrow = XR + (iy + ky - yr0) * G::XW + (ix0 - R - xr0);
+                const float* mrow = MR + (iy + ky - mr0y) * G::MW + (ix0 - R - mr0x);
+                uint32_t xs[kGfRun + 2 * R];
+                float ms[kGfRun + 2 * R];
+#pragma unroll
+                for (int t = 0; t < kGfRun + 2 * R; ++t) {
+                    xs[t] = xrow[t];
+                    ms[t] = mrow[t];
+                }
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) {
+#pragma unroll
+                    for (int j = 0; j < kGfRun; ++j) {
+                        const uint32_t p = xs[j + kx];
+                        s0[j] += p & 0xffu;
+                        s1[j] += (p >> 8) & 0xffu;
+                        s2[j] += (p >> 16) & 0xffu;
+                        const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);
+                        smax[j] = sb > smax[j] ? sb : smax[j];
+                        smin[j] = sb < smin[j] ? sb : smin[j];
+                        const float m = ms[j + kx];
+                        mmax[j] = mmax[j] < m ? m : mmax[j];
+                        msum[j] = msum[j] + m;  // row-major order, as the reference
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kGfRun; ++j) {
+                const int cx = clampi(ix0 + j, 0, W1), cy = clampi(iy, 0, H1);
+                for (int ky = -R; ky <= R; ++ky) {
+                    const uint32_t* xrow = XR + (cy + ky - yr0) * G::XW + (cx - xr0);
+                    const float* mrow = MR + (cy + ky - mr0y) * G::MW + (cx - mr0x);
+#pragma unroll
+                    for (int kx = -R; kx <= R; ++kx) {
+                        const uint32_t p = xrow[kx];
+                        s0[j] += p & 0xffu;
+                        s1[j] += (p >> 8) & 0xffu;
+                        s2[j] += (p >> 16) & 0xffu;
+                        const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);
+                        smax[j] = sb > smax[j] ? sb : smax[j];
+                        smin[j] = sb < smin[j] ? sb : smin[j];
+                        const float m = mrow[kx];
+                        mmax[j] = mmax[j] < m ? m : mmax[j];
+                        msum[j] = msum[j] + m;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kGfRun; ++j) {
+            const int i = py * G::BW + px0 + j;
+            BR[i] = (float)s0[j] / kk;
+            BR[G::BW * G::BH + i] = (float)s1[j] / kk;
+            BR[2 * G::BW * G::BH + i] = (float)s2[j] / kk;
+            const float imax = (float)(int)smax[j] / 3.f, imin = (float)(int)smin[j] / 3.f;
+            const float num = (imax - imin) * mmax[j];
+            RR[i] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+        }
+    }
+    __syncthreads();
+
+    // 4. guide: first strict argmin of rtv over the window (RR pre-clamped, so the
+    //    reference's clamped-coordinate scan is a direct row-major scan), alpha blend
+    const float sigma_alpha = 1.f / (float)(5 * K);
+    for (int run = tid; run < kGfTH * (kGfTW / kGfRun); run += kGfNT) {
+        const int ty = run / (kGfTW / kGfRun), tx0 = (run - ty * (kGfTW / kGfRun)) * kGfRun;
+        const int y = y0 + ty;
+        if (y > H1 || x0 + tx0 > W1) continue;
+        float rmin[kGfRun];
+        int mi[kGfRun];
+#pragma unroll
+        for (int j = 0; j < kGfRun; ++j) {
+            rmin[j] = CPP ? 3.402823466e+38f : 1e10f;
+            mi[j] = 0;
+        }
+        for (int ky = -R; ky <= R; ++ky) {
+            const int rowi = (ty + R + ky) * G::BW + tx0;  // BR/RR index of (x0+tx0-R, y+ky)
+            float rs[kGfRun + 2 * R];
+#pragma unroll
+            for (int t = 0; t < kGfRun + 2 * R; ++t) rs[t] = RR[rowi + t];
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) {
+#pragma unroll
+                for (int j = 0; j < kGfRun; ++j) {
+                    if (rmin[j] > rs[j + kx]) {
+                        rmin[j] = rs[j + kx];
+                        mi[j] = rowi + j + kx;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kGfRun; ++j) {
+            const int x = x0 + tx0 + j;
+            if (x > W1) break;
+            const int ci = (ty + R) * G::BW + tx0 + j + R;
+            const float arg = sigma_alpha * (RR[ci] - rmin[j]);
+            const float e = (float)exp((double)arg);
+            const float alpha = 2.f / (1.f + e) - 1.f;
+            const float beta = 1.f - alpha;
+            uint8_t* g = guide + ((long long)y * width + x) * 3;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const float bm = BR[c * G::BW * G::BH + mi[j]], bc = BR[c * G::BW * G::BH + ci];
+                const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
+                g[c] = (uint8_t)clampi((int)v, 0, 255);
+            }
+        }
+    }
+}
+
+template <int R, bool CPP>
+static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int height, int aligned, hipStream_t stream) {
+    constexpr int LDS = 4 * GfGeom<R>::WORDS;
+    static_assert(LDS <= kLdsBudget, "fused guide tile does not fit LDS");
+    auto kern = texture_guide_fused_kernel<R, CPP>;
+    static bool attr_done = false;
+    if (!attr_done) {
+        VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
+        attr_done = true;
+    }
+    dim3 grid((width + kGfTW - 1) / kGfTW, (height + kGfTH - 1) / kGfTH);
+    hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, height, aligned);
+    return (int)hipGetLastError();
+}
+
+template <bool CPP>
+static int launch_gf_r(int radius, const uint8_t* img, uint8_t* guide, int width, int height, int aligned,
+                       hipStream_t s) {
+    switch (radius) {
+        case 1: return launch_gf<1, CPP>(img, guide, width, height, aligned, s);
+        case 2: return launch_gf<2, CPP>(img, guide, width, height, aligned, s);
+        case 3: return launch_gf<3, CPP>(img, guide, width, height, aligned, s);
+        case 4: return launch_gf<4, CPP>(img, guide, width, height, aligned, s);
+        case 5: return launch_gf<5, CPP>(img, guide, width, height, aligned, s);
+        case 6: return launch_gf<6, CPP>(img, guide, width, height, aligned, s);
+        case 7: return launch_gf<7, CPP>(img, guide, width, height, aligned, s);
+        case 8: return launch_gf<8, CPP>(img, guide, width, height, aligned, s);
+        default: return VIP_ERR_UNSUPPORTED_KSIZE;
+    }
+}
+
+int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, bool cpp,
+                               hipStream_t stream) {
+    const int aligned = ((uintptr_t)img % 4 == 0) && ((size_t)width * 3 % 4 == 0);
+    return cpp ? launch_gf_r<true>(ksize / 2, img, guide, width, height, aligned, stream)
+               : launch_gf_r<false>(ksize / 2, img, guide, width, height, aligned, stream);
 }
 
 }  // namespace vip
