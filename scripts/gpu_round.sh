@@ -11,6 +11,8 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; ok $rc || exit $rc
 timeout -k 10 300 python bench.py > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_c2.json; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 ./samples/vip_benchmark 3840 2160 10 15 5 5 > gpurun_out/sample.log 2>&1
+rc=$?; echo "sample rc=$rc"; cat gpurun_out/sample.log | tail -6; [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python bench.py --steps 10 --no-cpu-baseline > gpurun_out/prof_c2.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; find gpurun_out/prof_c2 -name "*stats*" | head

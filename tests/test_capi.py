@@ -72,3 +72,14 @@ def test_cpp_headers_mirror_reference_signatures():
     assert "void bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst) const;" in hdr
     hdr = open(os.path.join(ROOT, "include", "cuda", "bilateral_texture_filter.hpp")).read()
     assert "void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst);" in hdr
+
+
+def test_sample_links_against_library():
+    """samples/vip_benchmark (C++ drop-in API consumer) is built and resolves libvip_hip.so."""
+    import subprocess
+    exe = os.path.join(ROOT, "samples", "vip_benchmark")
+    if not os.path.exists(exe):
+        pytest.skip("sample not built (make -C various_image_processings_amd/csrc samples)")
+    out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    line = [l for l in out.splitlines() if "libvip_hip" in l]
+    assert line and "not found" not in line[0]

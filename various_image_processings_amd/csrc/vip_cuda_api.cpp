@@ -3,7 +3,7 @@
 // (src/host_utilities.hpp:9-13): print "HIP Error <file> : <line> <message>" to
 // stderr and carry on; allocation failures in constructors throw
 // std::runtime_error (thrust::device_vector threw std::bad_alloc in the reference).
-#include <hip/hip_runtime.h>
+
 
 #include <cstdio>
 #include <stdexcept>
