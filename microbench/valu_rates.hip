@@ -16,16 +16,81 @@ __global__ __launch_bounds__(1024) void k(float* out, float a, float b) {
         for (int i = 0; i < 8; ++i) {
             if constexpr (KIND == 0) {
                 asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
-            } else if constexpr (KIND == 1) {
+            }
+            if constexpr (KIND == 1) {
                 asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[0]), "v"(*(double*)&x[2]));
-            } else if constexpr (KIND == 2) {
+            }
+            if constexpr (KIND == 2) {
                 asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
-            } else if constexpr (KIND == 3) {
-                asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
-            } else if constexpr (KIND == 4) {
-                asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(x[i]) : "v"(u[i]));
-            } else if constexpr (KIND == 5) {
+            }
+            if constexpr (KIND == 3) {
+                asm volatile("v_sad_u16 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+            }
+            if constexpr (KIND == 4) {
+                asm volatile("v_sad_u32 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+            }
+            if constexpr (KIND == 5) {
                 asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 6) {
+                asm volatile("v_lshlrev_b32 %0, 7, %0" : "+v"(u[i]));
+            }
+            if constexpr (KIND == 7) {
+                asm volatile("v_or_b32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 8) {
+                asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 9) {
+                asm volatile("v_mad_u32_u24 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 2) & 7]));
+            }
+            if constexpr (KIND == 10) {
+                asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 11) {
+                asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(x[i]) : "v"(u[i]));
+            }
+            if constexpr (KIND == 12) {
+                asm volatile("v_cvt_f32_u32 %0, %1" : "=v"(x[i]) : "v"(u[i]));
+            }
+            if constexpr (KIND == 13) {
+                asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+            }
+            if constexpr (KIND == 14) {
+                asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+            }
+            if constexpr (KIND == 15) {
+                asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[2]));
+            }
+            if constexpr (KIND == 16) {
+                asm volatile("v_pk_add_f32 %0, %1, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[2]));
+            }
+            if constexpr (KIND == 17) {
+                asm volatile("v_max_u32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 18) {
+                asm volatile("v_and_b32 %0, %0, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 19) {
+                asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(u[i]));
+            }
+            if constexpr (KIND == 20) {
+                asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 2) & 7]));
+            }
+            if constexpr (KIND == 21) {
+                asm volatile("v_dot4_u32_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+            }
+            if constexpr (KIND == 22) {
+                asm volatile("v_mov_b32 %0, %1" : "=v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 23) {
+                asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 24) {
+                asm volatile("v_max_f32 %0, %0, %1" : "+v"(x[i]) : "v"(x[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 25) {
+                asm volatile("v_sub_f32 %0, %0, %1" : "+v"(x[i]) : "v"(x[(i + 1) & 7]));
             }
         }
     }
@@ -46,7 +111,7 @@ double run(const char* name, float* d, int blocks, int pk) {
     float ms; hipEventElapsedTime(&ms, e0, e1);
     double insts = 5.0 * blocks * 16.0 /*waves*/ * ITERS * 8;  // wave-instructions
     double per_simd_cycles_ns = ms * 1e6 / (insts / (256.0 * 4));  // ns per wave-instr per SIMD
-    printf("%-16s %8.3f ms  %.3f ns per wave-instr per SIMD (= %.2f cycles at 2.4 GHz)%s\n", name, ms / 5, per_simd_cycles_ns,
+    printf("%-22s %8.3f ms  %.3f ns per wave-instr per SIMD (= %.2f cycles at 2.4 GHz)%s\n", name, ms / 5, per_simd_cycles_ns,
            per_simd_cycles_ns * 2.4, pk ? "  [2 f32 per lane]" : "");
     return ms;
 }
@@ -57,8 +122,28 @@ int main() {
     run<0>("v_fma_f32", d, blocks, 0);
     run<1>("v_pk_fma_f32", d, blocks, 1);
     run<2>("v_sad_u8", d, blocks, 0);
-    run<3>("v_mul_f32", d, blocks, 0);
-    run<4>("v_cvt_f32_ubyte1", d, blocks, 0);
+    run<3>("v_sad_u16", d, blocks, 0);
+    run<4>("v_sad_u32", d, blocks, 0);
     run<5>("v_lshl_or_b32", d, blocks, 0);
+    run<6>("v_lshlrev_b32 (VOP2)", d, blocks, 0);
+    run<7>("v_or_b32 (VOP2)", d, blocks, 0);
+    run<8>("v_add_u32 (VOP2)", d, blocks, 0);
+    run<9>("v_mad_u32_u24", d, blocks, 0);
+    run<10>("v_mul_u32_u24 (VOP2)", d, blocks, 0);
+    run<11>("v_cvt_f32_ubyte1", d, blocks, 0);
+    run<12>("v_cvt_f32_u32", d, blocks, 0);
+    run<13>("v_mul_f32", d, blocks, 0);
+    run<14>("v_add_f32", d, blocks, 0);
+    run<15>("v_pk_mul_f32", d, blocks, 1);
+    run<16>("v_pk_add_f32", d, blocks, 1);
+    run<17>("v_max_u32 (VOP2)", d, blocks, 0);
+    run<18>("v_and_b32 (VOP2)", d, blocks, 0);
+    run<19>("v_bfe_u32", d, blocks, 0);
+    run<20>("v_perm_b32", d, blocks, 0);
+    run<21>("v_dot4_u32_u8", d, blocks, 0);
+    run<22>("v_mov_b32", d, blocks, 0);
+    run<23>("v_cndmask_b32", d, blocks, 0);
+    run<24>("v_max_f32", d, blocks, 0);
+    run<25>("v_sub_f32", d, blocks, 0);
     return 0;
 }

@@ -103,7 +103,7 @@ def test_gradient(dev, oracle, ch, numerics, profile):
         assert np.array_equal(got, want), _mismatch(got, want)
 
 
-@pytest.mark.parametrize("k", [5, 9])
+@pytest.mark.parametrize("k", [4, 5, 9])
 @pytest.mark.parametrize("numerics,profile", PROFILES)
 def test_texture_stages_reference_inputs(dev, oracle, k, numerics, profile):
     """test/bilateral_texture_filter.cu:386-461 inputs; blur/rtv bit-exact, guide exact."""
@@ -123,7 +123,8 @@ def test_texture_stages_reference_inputs(dev, oracle, k, numerics, profile):
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
-@pytest.mark.parametrize("shape,k,nitr", [((48, 64), 5, 5), ((50, 50), 9, 3), ((121, 203), 5, 3), ((7, 9), 3, 2)])
+@pytest.mark.parametrize("shape,k,nitr", [((48, 64), 5, 5), ((50, 50), 9, 3), ((121, 203), 5, 3), ((7, 9), 3, 2),
+                                           ((40, 70), 4, 2), ((33, 65), 16, 1), ((90, 130), 15, 2)])
 @pytest.mark.parametrize("numerics,profile", PROFILES)
 def test_texture_end_to_end(dev, oracle, shape, k, nitr, numerics, profile):
     h, w = shape

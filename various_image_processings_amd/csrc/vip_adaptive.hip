@@ -109,9 +109,9 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
             }
 
             // ---- pass 2: offset-weighted bilateral over the disc ----
-            float s0[kP], s1[kP], s2[kP], sk[kP];
+            f2 a01[kP], a2k[kP];  // {sum_b, sum_g}, {sum_r, sumk}
         #pragma unroll
-            for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
+        for (int i = 0; i < kP; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
             for (int ky = -R; ky <= R; ++ky) {
                 const int aky = ky < 0 ? -ky : ky;
@@ -137,15 +137,12 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                         const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
                         return ((uint32_t)dist << 6) | lane16;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, gp, wsv, lut_bytes, widx, s0, s1, s2, sk);
+                    row_taps<HW, G::L, C0, 4 * NC, FMA, true>(gp, gp, wsv, lut_bytes, widx, a01, a2k);
                 });
             }
 
             uint32_t o[kP];
-        #pragma unroll
-            for (int i = 0; i < kP; ++i) {
-                o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) | (f2u8(s2[i] / sk[i] + 0.5f) << 16);
-            }
+        finish_outputs(a01, a2k, o);
             store8(a, ty0 + ty, tx0 + tx * kP, o);
         }
         if (next >= a.tiles_total) break;

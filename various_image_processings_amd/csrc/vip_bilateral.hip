@@ -80,9 +80,9 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                 ctr[0] = c0.x; ctr[1] = c0.y; ctr[2] = c0.z; ctr[3] = c0.w;
                 ctr[4] = c1.x; ctr[5] = c1.y; ctr[6] = c1.z; ctr[7] = c1.w;
             }
-            float s0[kP], s1[kP], s2[kP], sk[kP];
+            f2 a01[kP], a2k[kP];  // {sum_b, sum_g}, {sum_r, sumk}
 #pragma unroll
-            for (int i = 0; i < kP; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
+for (int i = 0; i < kP; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
             for (int ky = -R; ky <= R; ++ky) {
                 const int aky = ky < 0 ? -ky : ky;
@@ -110,16 +110,12 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                     auto widx = [&](uint32_t g, float, float, float, int i) {
                         return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << 7) | lane4;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA>(gp, sp, wsv, lut_bytes, widx, s0, s1, s2, sk);
+                    row_taps<HW, G::L, C0, 4 * NC, FMA, false>(gp, sp, wsv, lut_bytes, widx, a01, a2k);
                 });
             }
 
             uint32_t o[kP];
-#pragma unroll
-            for (int i = 0; i < kP; ++i) {
-                o[i] = f2u8(s0[i] / sk[i] + 0.5f) | (f2u8(s1[i] / sk[i] + 0.5f) << 8) |
-                       (f2u8(s2[i] / sk[i] + 0.5f) << 16);
-            }
+finish_outputs(a01, a2k, o);
             store8(a, ty0 + ty, tx0 + tx * kP, o);
         }
         VIP_STAMP(it, 1);

@@ -62,10 +62,12 @@ struct Geom {
     static constexpr int GROUPS = (kTW + 2 * L) / 4;        // 4-pixel groups per tile row
 };
 
-// Largest wave count (<= MAXW: 16, 8 or 4) whose LUT + plane(s) fit the CU's LDS.
+// Largest wave count (<= MAXW: 16, 12, 8 or 4) whose LUT + plane(s) fit the CU's LDS.
 template <int R, int PLANES, int MAXW = 16>
 constexpr int pick_waves() {
-    for (int w = MAXW; w >= 4; w /= 2) {
+    constexpr int cand[4] = {16, 12, 8, 4};
+    for (int w : cand) {
+        if (w > MAXW) continue;
         const long long bytes = 4LL * lut_words(false) + 4LL * PLANES * (w * 4 + 2 * R) * Geom<R>::S;
         if (bytes <= kLdsBudget) return w;
     }
@@ -226,28 +228,34 @@ __device__ __forceinline__ void set_progress_priority(int band) {
 // `widx(g, f0, f1, f2, i)` returns the LDS byte address of the colour weight of
 // guide word g (source floats f*) for output i. Accumulation order per output is
 // ascending kx, as in the reference's row-major loop.
-template <int HW, int L, int C0, int NGP, bool FMA, class WIdx>
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// PK: accumulate with v_pk_fma_f32 ({s0,s1} and {s2,sk} pairs). Measured on gfx950:
+// +3 % for the adaptive kernel, -10 % for the bilateral kernel (the {r, 1} pairs
+// push it past 128 VGPRs), so it is a per-kernel choice.
+template <int HW, int L, int C0, int NGP, bool FMA, bool PK, class WIdx>
 __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32_t (&sp)[NGP],
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
-                                         float (&s0)[kP], float (&s1)[kP], float (&s2)[kP], float (&sk)[kP]) {
+                                         f2 (&a01)[kP], f2 (&a2k)[kP]) {
     constexpr int D = VIP_PIPE_DEPTH;
     constexpr int NB = D + 1;            // ring of in-flight columns
     constexpr int J0 = L - HW;           // first neighbour column relative to the thread's 8
     constexpr int J1 = L + kP - 1 + HW;  // last
     float wc[NB][kP];
-    float nf[NB][3];
+    f2 n01[NB], n21[NB];                 // {b, g} and {r, 1} of the neighbour (source image)
     auto issue = [&](int j) {
         const uint32_t g = gp[j - 4 * C0];
         const uint32_t p = sp[j - 4 * C0];
-        float* f = nf[(j - J0) % NB];
-        f[0] = (float)(p & 0xffu);
-        f[1] = (float)((p >> 8) & 0xffu);
-        f[2] = (float)((p >> 16) & 0xffu);
+        const int b = (j - J0) % NB;
+        n01[b].x = (float)(p & 0xffu);
+        n01[b].y = (float)((p >> 8) & 0xffu);
+        n21[b].x = (float)((p >> 16) & 0xffu);
+        n21[b].y = 1.0f;
 #pragma unroll
         for (int i = 0; i < kP; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            wc[(j - J0) % NB][i] = *reinterpret_cast<const float*>(lut + widx(g, f[0], f[1], f[2], i));
+            wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b].x, n01[b].y, n21[b].x, i));
         }
     };
 #pragma unroll
@@ -255,26 +263,42 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
 #pragma unroll
     for (int j = J0; j <= J1; ++j) {
         if (j + D <= J1) issue(j + D);
-        const float* f = nf[(j - J0) % NB];
+        const int b = (j - J0) % NB;
 #pragma unroll
         for (int i = 0; i < kP; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            const float w = wc[(j - J0) % NB][i] * wsv[kx < 0 ? -kx : kx];
-            if constexpr (FMA) {
-                s0[i] = __builtin_fmaf(f[0], w, s0[i]);
-                s1[i] = __builtin_fmaf(f[1], w, s1[i]);
-                s2[i] = __builtin_fmaf(f[2], w, s2[i]);
+            const float w = wc[b][i] * wsv[kx < 0 ? -kx : kx];
+            if constexpr (FMA && PK) {
+                // v_pk_fma_f32: {s0,s1} += {b,g}*w and {s2,sk} += {r,1}*w; each half is an
+                // IEEE fma, and fma(1, w, sk) == sk + w exactly
+                const f2 w2 = {w, w};
+                a01[i] = __builtin_elementwise_fma(n01[b], w2, a01[i]);
+                a2k[i] = __builtin_elementwise_fma(n21[b], w2, a2k[i]);
+            } else if constexpr (FMA) {
+                a01[i].x = __builtin_fmaf(n01[b].x, w, a01[i].x);
+                a01[i].y = __builtin_fmaf(n01[b].y, w, a01[i].y);
+                a2k[i].x = __builtin_fmaf(n21[b].x, w, a2k[i].x);
+                a2k[i].y = a2k[i].y + w;
             } else {
-                s0[i] = s0[i] + f[0] * w;
-                s1[i] = s1[i] + f[1] * w;
-                s2[i] = s2[i] + f[2] * w;
+                a01[i].x = a01[i].x + n01[b].x * w;
+                a01[i].y = a01[i].y + n01[b].y * w;
+                a2k[i].x = a2k[i].x + n21[b].x * w;
+                a2k[i].y = a2k[i].y + w;
             }
-            sk[i] = sk[i] + w;
         }
 #ifndef VIP_NO_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);
 #endif
+    }
+}
+
+// dst = u8(sum_c / sumk + 0.5f) for the kP outputs, packed as RGBX words
+__device__ __forceinline__ void finish_outputs(const f2 (&a01)[kP], const f2 (&a2k)[kP], uint32_t (&o)[kP]) {
+#pragma unroll
+    for (int i = 0; i < kP; ++i) {
+        const float sk = a2k[i].y;
+        o[i] = f2u8(a01[i].x / sk + 0.5f) | (f2u8(a01[i].y / sk + 0.5f) << 8) | (f2u8(a2k[i].x / sk + 0.5f) << 16);
     }
 }
 

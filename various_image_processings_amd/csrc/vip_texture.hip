@@ -115,12 +115,14 @@ __global__ __launch_bounds__(256) void blur_rtv_kernel(const uint8_t* __restrict
     // channel sums are exact integers (== the reference's float sums, all < 2^24);
     // intensity extremes come from integer byte sums: x -> float(x)/3.f is monotonic,
     // so max_i(s_i/3.f) == (max_i s_i)/3.f and one divide replaces k*k of them
+    // window 2*(ksize/2)+1 wide; the divisor below is ksize^2 even for even ksize
+    const int kw = 2 * radius + 1;
     uint32_t s0 = 0, s1 = 0, s2 = 0, smax = 0, smin = 0xffffffffu;
     float mmax = 0.f, msum = 0.f;
-    for (int ky = 0; ky < ksize; ++ky) {
+    for (int ky = 0; ky < kw; ++ky) {
         const uint32_t* ri = s_img + (ty + ky) * tw + tx;
         const float* rm = s_mag + (ty + ky) * tw + tx;
-        for (int kx = 0; kx < ksize; ++kx) {
+        for (int kx = 0; kx < kw; ++kx) {
             const uint32_t p = ri[kx];
             s0 += p & 0xffu;
             s1 += (p >> 8) & 0xffu;
@@ -181,9 +183,10 @@ __global__ __launch_bounds__(256) void guide_kernel(const float* __restrict__ bl
     // CUDA initialises with 1e10f (:152), include/cpp with FLT_MAX (:97)
     float rmin = CPP ? 3.402823466e+38f : 1e10f;
     int mx = 0, my = 0;
-    for (int ky = 0; ky < ksize; ++ky) {
+    const int kw = 2 * radius + 1;  // window; sigma_alpha below uses ksize (even ksize too)
+    for (int ky = 0; ky < kw; ++ky) {
         const float* rr = s_rtv + (ty + ky) * tw + tx;
-        for (int kx = 0; kx < ksize; ++kx) {
+        for (int kx = 0; kx < kw; ++kx) {
             const float v = rr[kx];
             if (rmin > v) {
                 rmin = v;
@@ -262,9 +265,11 @@ struct GfGeom {
 template <int R, bool CPP>
 __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
                                                                    uint8_t* __restrict__ guide, int width,
-                                                                   int height, int aligned) {
+                                                                   int height, int ksize, int aligned) {
     using G = GfGeom<R>;
-    constexpr int K = 2 * R + 1;
+    constexpr int K = 2 * R + 1;  // window width; the reference divides by ksize^2 and
+                                  // uses sigma_alpha = 1/(5 ksize) even when ksize is even
+    constexpr bool PACKRB = K * K * 255 < 65536;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* XR = lds;
     float* MR = reinterpret_cast<float*>(XR + G::XW * G::XH);
@@ -317,11 +322,11 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     __syncthreads();
 
     // 3. box blur + mRTV, kGfRun horizontally adjacent positions per thread
-    const float kk = (float)(K * K);
+    const float kk = (float)(ksize * ksize);
     for (int run = tid; run < G::BH * (G::BW / kGfRun); run += kGfNT) {
         const int py = run / (G::BW / kGfRun), px0 = (run - py * (G::BW / kGfRun)) * kGfRun;
         const int iy = br0y + py, ix0 = br0x + px0;
-        uint32_t s0[kGfRun], s1[kGfRun], s2[kGfRun], smax[kGfRun], smin[kGfRun];
+        uint32_t s0[kGfRun], s1[kGfRun], smax[kGfRun], smin[kGfRun], s2[kGfRun];
         float mmax[kGfRun], msum[kGfRun];
 #pragma unroll
         for (int j = 0; j < kGfRun; ++j) {
@@ -346,14 +351,18 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 #pragma unroll
                     for (int j = 0; j < kGfRun; ++j) {
                         const uint32_t p = xs[j + kx];
-                        s0[j] += p & 0xffu;
-                        s1[j] += (p >> 8) & 0xffu;
-                        s2[j] += (p >> 16) & 0xffu;
+                        if constexpr (PACKRB) {
+                            s0[j] += p & 0x00ff00ffu;  // R | B<<16 in 16-bit lanes
+                        } else {
+                            s0[j] += p & 0xffu;
+                            s2[j] += __builtin_amdgcn_ubfe(p, 16, 8);
+                        }
+                        s1[j] += __builtin_amdgcn_ubfe(p, 8, 8);
                         const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);
                         smax[j] = sb > smax[j] ? sb : smax[j];
                         smin[j] = sb < smin[j] ? sb : smin[j];
                         const float m = ms[j + kx];
-                        mmax[j] = mmax[j] < m ? m : mmax[j];
+                        mmax[j] = __builtin_fmaxf(mmax[j], m);  // == the reference's max for non-NaN
                         msum[j] = msum[j] + m;  // row-major order, as the reference
                     }
                 }
@@ -368,14 +377,18 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 #pragma unroll
                     for (int kx = -R; kx <= R; ++kx) {
                         const uint32_t p = xrow[kx];
-                        s0[j] += p & 0xffu;
-                        s1[j] += (p >> 8) & 0xffu;
-                        s2[j] += (p >> 16) & 0xffu;
+                        if constexpr (PACKRB) {
+                            s0[j] += p & 0x00ff00ffu;  // R | B<<16 in 16-bit lanes
+                        } else {
+                            s0[j] += p & 0xffu;
+                            s2[j] += __builtin_amdgcn_ubfe(p, 16, 8);
+                        }
+                        s1[j] += __builtin_amdgcn_ubfe(p, 8, 8);
                         const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);
                         smax[j] = sb > smax[j] ? sb : smax[j];
                         smin[j] = sb < smin[j] ? sb : smin[j];
                         const float m = mrow[kx];
-                        mmax[j] = mmax[j] < m ? m : mmax[j];
+                        mmax[j] = __builtin_fmaxf(mmax[j], m);
                         msum[j] = msum[j] + m;
                     }
                 }
@@ -384,9 +397,9 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 #pragma unroll
         for (int j = 0; j < kGfRun; ++j) {
             const int i = py * G::BW + px0 + j;
-            BR[i] = (float)s0[j] / kk;
+            BR[i] = (float)(PACKRB ? (s0[j] & 0xffffu) : s0[j]) / kk;
             BR[G::BW * G::BH + i] = (float)s1[j] / kk;
-            BR[2 * G::BW * G::BH + i] = (float)s2[j] / kk;
+            BR[2 * G::BW * G::BH + i] = (float)(PACKRB ? (s0[j] >> 16) : s2[j]) / kk;
             const float imax = (float)(int)smax[j] / 3.f, imin = (float)(int)smin[j] / 3.f;
             const float num = (imax - imin) * mmax[j];
             RR[i] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
@@ -394,49 +407,55 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     }
     __syncthreads();
 
-    // 4. guide: first strict argmin of rtv over the window (RR pre-clamped, so the
-    //    reference's clamped-coordinate scan is a direct row-major scan), alpha blend
-    const float sigma_alpha = 1.f / (float)(5 * K);
-    for (int run = tid; run < kGfTH * (kGfTW / kGfRun); run += kGfNT) {
-        const int ty = run / (kGfTW / kGfRun), tx0 = (run - ty * (kGfTW / kGfRun)) * kGfRun;
-        const int y = y0 + ty;
-        if (y > H1 || x0 + tx0 > W1) continue;
-        float rmin[kGfRun];
-        int mi[kGfRun];
+    // 4. guide: first strict argmin of rtv over the window (RR is pre-clamped, so the
+    //    reference's clamped-coordinate scan is a direct row-major scan). A thread
+    //    takes kGfRun vertically adjacent outputs: each window row's first argmin is
+    //    found once and shared; scanning those rows in order with strict > then
+    //    gives the row-major first argmin. Alpha blend per output.
+    const float sigma_alpha = 1.f / (float)(5 * ksize);
+    for (int run = tid; run < (kGfTH / kGfRun) * kGfTW; run += kGfNT) {
+        const int tx = run % kGfTW, ty0 = (run / kGfTW) * kGfRun;
+        const int x = x0 + tx;
+        if (x > W1 || y0 + ty0 > H1) continue;
+        float rv[kGfRun + 2 * R];
+        int ri[kGfRun + 2 * R];
 #pragma unroll
-        for (int j = 0; j < kGfRun; ++j) {
-            rmin[j] = CPP ? 3.402823466e+38f : 1e10f;
-            mi[j] = 0;
-        }
-        for (int ky = -R; ky <= R; ++ky) {
-            const int rowi = (ty + R + ky) * G::BW + tx0;  // BR/RR index of (x0+tx0-R, y+ky)
-            float rs[kGfRun + 2 * R];
+        for (int t = 0; t < kGfRun + 2 * R; ++t) {  // window rows ty0-R .. ty0+kGfRun-1+R
+            const float* row = RR + (ty0 + t) * G::BW + tx;
+            float v = row[0];
+            int c = 0;
 #pragma unroll
-            for (int t = 0; t < kGfRun + 2 * R; ++t) rs[t] = RR[rowi + t];
-#pragma unroll
-            for (int kx = 0; kx < K; ++kx) {
-#pragma unroll
-                for (int j = 0; j < kGfRun; ++j) {
-                    if (rmin[j] > rs[j + kx]) {
-                        rmin[j] = rs[j + kx];
-                        mi[j] = rowi + j + kx;
-                    }
+            for (int kx = 1; kx < K; ++kx) {
+                if (v > row[kx]) {
+                    v = row[kx];
+                    c = kx;
                 }
             }
+            rv[t] = v;
+            ri[t] = (ty0 + t) * G::BW + tx + c;
         }
 #pragma unroll
         for (int j = 0; j < kGfRun; ++j) {
-            const int x = x0 + tx0 + j;
-            if (x > W1) break;
-            const int ci = (ty + R) * G::BW + tx0 + j + R;
-            const float arg = sigma_alpha * (RR[ci] - rmin[j]);
+            const int y = y0 + ty0 + j;
+            if (y > H1) break;
+            float rmin = CPP ? 3.402823466e+38f : 1e10f;
+            int mi = 0;
+#pragma unroll
+            for (int ky = 0; ky < K; ++ky) {
+                if (rmin > rv[j + ky]) {
+                    rmin = rv[j + ky];
+                    mi = ri[j + ky];
+                }
+            }
+            const int ci = (ty0 + j + R) * G::BW + tx + R;
+            const float arg = sigma_alpha * (RR[ci] - rmin);
             const float e = (float)exp((double)arg);
             const float alpha = 2.f / (1.f + e) - 1.f;
             const float beta = 1.f - alpha;
             uint8_t* g = guide + ((long long)y * width + x) * 3;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const float bm = BR[c * G::BW * G::BH + mi[j]], bc = BR[c * G::BW * G::BH + ci];
+                const float bm = BR[c * G::BW * G::BH + mi], bc = BR[c * G::BW * G::BH + ci];
                 const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
                 g[c] = (uint8_t)clampi((int)v, 0, 255);
             }
@@ -445,7 +464,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 }
 
 template <int R, bool CPP>
-static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int height, int aligned, hipStream_t stream) {
+static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, int aligned,
+                     hipStream_t stream) {
     constexpr int LDS = 4 * GfGeom<R>::WORDS;
     static_assert(LDS <= kLdsBudget, "fused guide tile does not fit LDS");
     auto kern = texture_guide_fused_kernel<R, CPP>;
@@ -456,22 +476,22 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int height, 
         attr_done = true;
     }
     dim3 grid((width + kGfTW - 1) / kGfTW, (height + kGfTH - 1) / kGfTH);
-    hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, height, aligned);
+    hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, height, ksize, aligned);
     return (int)hipGetLastError();
 }
 
 template <bool CPP>
-static int launch_gf_r(int radius, const uint8_t* img, uint8_t* guide, int width, int height, int aligned,
+static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width, int height, int aligned,
                        hipStream_t s) {
-    switch (radius) {
-        case 1: return launch_gf<1, CPP>(img, guide, width, height, aligned, s);
-        case 2: return launch_gf<2, CPP>(img, guide, width, height, aligned, s);
-        case 3: return launch_gf<3, CPP>(img, guide, width, height, aligned, s);
-        case 4: return launch_gf<4, CPP>(img, guide, width, height, aligned, s);
-        case 5: return launch_gf<5, CPP>(img, guide, width, height, aligned, s);
-        case 6: return launch_gf<6, CPP>(img, guide, width, height, aligned, s);
-        case 7: return launch_gf<7, CPP>(img, guide, width, height, aligned, s);
-        case 8: return launch_gf<8, CPP>(img, guide, width, height, aligned, s);
+    switch (ksize / 2) {
+        case 1: return launch_gf<1, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 2: return launch_gf<2, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 3: return launch_gf<3, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 4: return launch_gf<4, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 5: return launch_gf<5, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 6: return launch_gf<6, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 7: return launch_gf<7, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 8: return launch_gf<8, CPP>(img, guide, width, height, ksize, aligned, s);
         default: return VIP_ERR_UNSUPPORTED_KSIZE;
     }
 }
@@ -479,8 +499,8 @@ static int launch_gf_r(int radius, const uint8_t* img, uint8_t* guide, int width
 int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, bool cpp,
                                hipStream_t stream) {
     const int aligned = ((uintptr_t)img % 4 == 0) && ((size_t)width * 3 % 4 == 0);
-    return cpp ? launch_gf_r<true>(ksize / 2, img, guide, width, height, aligned, stream)
-               : launch_gf_r<false>(ksize / 2, img, guide, width, height, aligned, stream);
+    return cpp ? launch_gf_r<true>(ksize, img, guide, width, height, aligned, stream)
+               : launch_gf_r<false>(ksize, img, guide, width, height, aligned, stream);
 }
 
 }  // namespace vip
