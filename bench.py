@@ -115,6 +115,7 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        dist.barrier()  # communicator up before the first (P2P) halo exchange
 
     import various_image_processings_amd as vip
     from various_image_processings_amd.filters import _TextureImpl

@@ -92,6 +92,49 @@ __global__ __launch_bounds__(1024) void k(float* out, float a, float b) {
             if constexpr (KIND == 25) {
                 asm volatile("v_sub_f32 %0, %0, %1" : "+v"(x[i]) : "v"(x[(i + 1) & 7]));
             }
+            if constexpr (KIND == 26) {
+                asm volatile("v_add_f32_e64 %0, |%0|, |%1|" : "+v"(x[i]) : "v"(x[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 27) {
+                asm volatile("v_cvt_u32_f32 %0, %1" : "=v"(u[i]) : "v"(x[i]));
+            }
+            if constexpr (KIND == 28) {
+                asm volatile("v_lshl_add_u32 %0, %0, 6, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+            }
+            if constexpr (KIND == 29) {
+                asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(x[i]) : "v"(a), "v"(b));
+            }
+            if constexpr (KIND == 30) {
+                asm volatile("v_pk_add_f32 %0, %0, %1 neg_lo:[0,1] neg_hi:[0,1]" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[2]));
+            }
+            if constexpr (KIND == 31) {  // sad + fma alternating (slow + fast)
+                if (i & 1) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+                else asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+            }
+            if constexpr (KIND == 32) {  // lshl_or + mul alternating
+                if (i & 1) asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7]));
+                else asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+            }
+            if constexpr (KIND == 33) {  // bilateral pair: sad, lshl_or, mul, 3 fma, add + 1 fma (8 instrs)
+                switch (i) {
+                    case 0: asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[0]) : "v"(u[1]), "v"(u[3])); break;
+                    case 1: asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(u[2]) : "v"(u[5])); break;
+                    case 2: asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[0]) : "v"(a)); break;
+                    case 3: asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[1]) : "v"(a), "v"(b)); break;
+                    case 4: asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[2]) : "v"(a), "v"(b)); break;
+                    case 5: asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[3]) : "v"(a), "v"(b)); break;
+                    case 6: asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[4]) : "v"(a)); break;
+                    default: asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[5]) : "v"(a), "v"(b)); break;
+                }
+            }
+            if constexpr (KIND == 34) {  // two slow ops alternating: cvt_f32_ubyte + sad
+                if (i & 1) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+                else asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(x[i]) : "v"(u[i]));
+            }
+            if constexpr (KIND == 35) {  // 1 slow : 3 fast
+                if ((i & 3) == 0) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+                else asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+            }
         }
     }
     float s = 0;
@@ -145,5 +188,15 @@ int main() {
     run<23>("v_cndmask_b32", d, blocks, 0);
     run<24>("v_max_f32", d, blocks, 0);
     run<25>("v_sub_f32", d, blocks, 0);
+    run<26>("v_add_f32_e64 |a|+|b|", d, blocks, 0);
+    run<27>("v_cvt_u32_f32", d, blocks, 0);
+    run<28>("v_lshl_add_u32", d, blocks, 0);
+    run<29>("v_fmac_f32 (VOP2)", d, blocks, 0);
+    run<30>("v_pk_add_f32 neg", d, blocks, 1);
+    run<31>("mix sad/fma 1:1", d, blocks, 0);
+    run<32>("mix lshl_or/mul 1:1", d, blocks, 0);
+    run<33>("mix bilateral pair 8", d, blocks, 0);
+    run<34>("mix cvt/sad 1:1", d, blocks, 0);
+    run<35>("mix sad/fma 1:3", d, blocks, 0);
     return 0;
 }

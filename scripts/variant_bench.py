@@ -10,14 +10,20 @@ import sys, json, torch, ctypes
 sys.path.insert(0, ".")
 import various_image_processings_amd._lib as L
 L.LIB_PATH = sys.argv[1]
-from various_image_processings_amd.filters import _BilateralImpl, _AdaptiveImpl
+from various_image_processings_amd.filters import _BilateralImpl, _AdaptiveImpl, _TextureImpl
 torch.cuda.set_device(0)
 W, H = 3840, 2160
 srcs = [torch.randint(0, 255, (H, W, 3), dtype=torch.uint8, device="cuda") for _ in range(6)]
 dst = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda")
 res = {}
-for name, impl, fn in (("bilateral", _BilateralImpl(W, H, 15), "bilateral_filter"), ("adaptive", _AdaptiveImpl(W, H, 15), "execute")):
-    f = getattr(impl, fn)
+guide = srcs[5]
+cases = [("bilateral", _BilateralImpl(W, H, 15).bilateral_filter),
+         ("adaptive", _AdaptiveImpl(W, H, 15).execute)]
+j9, j15 = _BilateralImpl(W, H, 9), _BilateralImpl(W, H, 15)
+cases += [("joint_r4", lambda s, d: j9.joint_bilateral_filter(s, guide, d)),
+          ("joint_r7", lambda s, d: j15.joint_bilateral_filter(s, guide, d)),
+          ("texture_k5_nitr1", _TextureImpl(W, H, 5, 1).execute)]
+for name, f in cases:
     for i in range(3): f(srcs[i % 6], dst)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

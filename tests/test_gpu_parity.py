@@ -62,13 +62,23 @@ def test_bilateral_large_frame(dev, oracle, k, ss, sc):
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
-@pytest.mark.parametrize("k", [3, 9, 15])
+@pytest.mark.parametrize("k", [3, 9, 15, 25, 31])
 @pytest.mark.parametrize("numerics,profile", PROFILES)
 def test_joint_bilateral(dev, oracle, k, numerics, profile):
     img = oracle.random_image(70, 45)
     guide = oracle.random_u8(70 * 45 * 3)[::-1].copy().reshape(45, 70, 3)
     got = _bilateral_gpu(dev, img, k, numerics=numerics, guide=guide)
     want = oracle.joint_bilateral(img, guide, k, profile=profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("k", [9, 25])
+def test_joint_bilateral_multi_tile(dev, oracle, k):
+    # several persistent tiles per workgroup in both directions (joint kernel: 2 planes)
+    img = oracle.random_image(700, 530)
+    guide = oracle.random_u8(700 * 530 * 3)[::-1].copy().reshape(530, 700, 3)
+    got = _bilateral_gpu(dev, img, k, guide=guide)
+    want = oracle.joint_bilateral(img, guide, k, threads=8)
     assert np.array_equal(got, want), _mismatch(got, want)
 
 

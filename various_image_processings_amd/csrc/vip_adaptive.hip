@@ -13,19 +13,23 @@
 // packed R|B lanes when (2R+1)^2*255 < 2^16), then a horizontal sliding window.
 #include "vip_stencil.hpp"
 
+#ifndef VIP_ADA_P
+#define VIP_ADA_P 4
+#endif
+
 namespace vip {
 
-template <int R, int WAVES, bool FMA>
+template <int R, int WAVES, bool FMA, int P>
 __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs a) {
-    using G = Geom<R>;
+    using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
     constexpr int TH = WAVES * 4;
     constexpr int ROWS = TH + 2 * R;
     constexpr int K = 2 * R + 1;
     constexpr bool PACK = K * K * 255 < 65536;
-    constexpr int NCOL = kP + 2 * R;           // columns touched by the thread's 8 windows
-    constexpr int JB = G::L - R;               // first column relative to tx*8
-    constexpr int CB0 = JB / 4, CB1 = (G::L + kP - 1 + R) / 4;
+    constexpr int NCOL = P + 2 * R;            // columns touched by the thread's P windows
+    constexpr int JB = G::L - R;               // first column relative to tx*P
+    constexpr int CB0 = JB / 4, CB1 = (G::L + P - 1 + R) / 4;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
     uint32_t* const plane = lds + lut_words(true);
@@ -39,69 +43,97 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x
-    TilePrefetch<R, ROWS, NT> pf;
-    pf.issue(a.src, a.src_pitch, a, (tile % a.tiles_x) * kTW, (tile / a.tiles_x) * TH);
-    stage_lut<NT, 1536>(lut, a.color);
+    TilePrefetch<R, ROWS, NT, P> pf;
+    {
+        const int mt = xcd_tile(tile, a.tiles_total);
+        pf.issue(a.src, a.src_pitch, a, (mt % a.tiles_x) * G::TW, (mt / a.tiles_x) * TH);
+    }
+    stage_lut<NT, 1536, 16>(lut, a.color);
     pf.commit(plane);
     __syncthreads();
 
     while (true) {
-        const int tx0 = (tile % a.tiles_x) * kTW, ty0 = (tile / a.tiles_x) * TH;
+        const int mt = xcd_tile(tile, a.tiles_total);
+        const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
-        if (next < a.tiles_total) pf.issue(a.src, a.src_pitch, a, (next % a.tiles_x) * kTW, (next / a.tiles_x) * TH);
+        if (next < a.tiles_total) {
+            const int mn = xcd_tile(next, a.tiles_total);
+            pf.issue(a.src, a.src_pitch, a, (mn % a.tiles_x) * G::TW, (mn / a.tiles_x) * TH);
+        }
         if (ty0 + wave * 4 < a.out_rows) {
             // ---- pass 1: box sums over the full square ----
-            uint32_t vrb[NCOL], vg[NCOL], vb[PACK ? 1 : NCOL];
+            // Column sums are kept only for the columns the sliding window adds or
+            // drops (slot j < P-1 and j >= K); the window's other columns go straight
+            // into one running sum, so registers stay O(P), not O(P + 2R).
+            constexpr int HI0 = (K > P - 1) ? K : P - 1;     // first column with a "hi" slot
+            constexpr int NSLOT = (P - 1) + (K + P - 1 - HI0);
+            auto slot = [](int j) constexpr { return j < P - 1 ? j : (j >= HI0 ? P - 1 + j - HI0 : -1); };
+            uint32_t vrb[NSLOT], vg[NSLOT], vb[PACK ? 1 : NSLOT];
+            uint32_t mrb = 0u, mg = 0u, mb = 0u;            // columns in [P-1, K) without a slot
         #pragma unroll
-            for (int j = 0; j < NCOL; ++j) { vrb[j] = 0u; vg[j] = 0u; if constexpr (!PACK) vb[j] = 0u; }
+            for (int q = 0; q < NSLOT; ++q) { vrb[q] = 0u; vg[q] = 0u; if constexpr (!PACK) vb[q] = 0u; }
             for (int r = 0; r < K; ++r) {
-                const uint32_t* row = plane + (ty + r) * G::S + tx * kP;
-                uint32_t px[4 * (CB1 - CB0 + 1)];
+                const uint32_t* row = plane + (ty + r) * G::S + tx * P;
         #pragma unroll
                 for (int c = CB0; c <= CB1; ++c) {
-                    const uint4 q = *reinterpret_cast<const uint4*>(row + 4 * c);
-                    px[4 * (c - CB0) + 0] = q.x; px[4 * (c - CB0) + 1] = q.y;
-                    px[4 * (c - CB0) + 2] = q.z; px[4 * (c - CB0) + 3] = q.w;
-                }
+                    const uint4 q4 = *reinterpret_cast<const uint4*>(row + 4 * c);
+                    const uint32_t w4[4] = {q4.x, q4.y, q4.z, q4.w};
         #pragma unroll
-                for (int j = 0; j < NCOL; ++j) {
-                    const uint32_t p = px[JB + j - 4 * CB0];
-                    if constexpr (PACK) {
-                        vrb[j] += p & 0x00ff00ffu;
-                        vg[j] += (p >> 8) & 0xffu;
-                    } else {
-                        vrb[j] += p & 0xffu;
-                        vg[j] += (p >> 8) & 0xffu;
-                        vb[j] += (p >> 16) & 0xffu;
+                    for (int t = 0; t < 4; ++t) {
+                        const int j = 4 * c + t - JB;  // window column of this word
+                        if (j < 0 || j >= NCOL) continue;
+                        const uint32_t p = w4[t];
+                        const int q = slot(j);
+                        uint32_t& arb = q >= 0 ? vrb[q < 0 ? 0 : q] : mrb;
+                        uint32_t& ag = q >= 0 ? vg[q < 0 ? 0 : q] : mg;
+                        if constexpr (PACK) {
+                            arb += p & 0x00ff00ffu;
+                            ag += (p >> 8) & 0xffu;
+                        } else {
+                            uint32_t& ab = q >= 0 ? vb[q < 0 ? 0 : q] : mb;
+                            arb += p & 0xffu;
+                            ag += (p >> 8) & 0xffu;
+                            ab += (p >> 16) & 0xffu;
+                        }
                     }
                 }
             }
-            uint32_t ctr[kP];
-            float c0f[kP], c1f[kP], c2f[kP], o0[kP], o1[kP], o2[kP];
+            uint32_t ctr[P];
+            float c0f[P], c1f[P], c2f[P], o0[P], o1[P], o2[P];
             {
-                const uint32_t* c = plane + (ty + R) * G::S + tx * kP + G::L;
-                const uint4 q0 = *reinterpret_cast<const uint4*>(c);
-                const uint4 q1 = *reinterpret_cast<const uint4*>(c + 4);
-                ctr[0] = q0.x; ctr[1] = q0.y; ctr[2] = q0.z; ctr[3] = q0.w;
-                ctr[4] = q1.x; ctr[5] = q1.y; ctr[6] = q1.z; ctr[7] = q1.w;
+                const uint4* c = reinterpret_cast<const uint4*>(plane + (ty + R) * G::S + tx * P + G::L);
+        #pragma unroll
+                for (int q = 0; q < P / 4; ++q) {
+                    const uint4 v = c[q];
+                    ctr[4 * q + 0] = v.x; ctr[4 * q + 1] = v.y; ctr[4 * q + 2] = v.z; ctr[4 * q + 3] = v.w;
+                }
             }
             {
-                uint32_t wrb = 0u, wg = 0u, wb = 0u;
+                uint32_t wrb = mrb, wg = mg, wb = mb;
         #pragma unroll
-                for (int j = 0; j < K; ++j) { wrb += vrb[j]; wg += vg[j]; if constexpr (!PACK) wb += vb[j]; }
+                for (int j = 0; j < K; ++j) {
+                    const int q = slot(j);
+                    if (q < 0) continue;
+                    wrb += vrb[q]; wg += vg[q]; if constexpr (!PACK) wb += vb[q];
+                }
                 const float kk = (float)(K * K);
         #pragma unroll
-                for (int i = 0; i < kP; ++i) {
+                for (int i = 0; i < P; ++i) {
                     if (i > 0) {
-                        wrb += vrb[i + K - 1] - vrb[i - 1];
-                        wg += vg[i + K - 1] - vg[i - 1];
-                        if constexpr (!PACK) wb += vb[i + K - 1] - vb[i - 1];
+                        const int qa = slot(i + K - 1), qd = slot(i - 1);
+                        wrb += vrb[qa] - vrb[qd];
+                        wg += vg[qa] - vg[qd];
+                        if constexpr (!PACK) wb += vb[qa] - vb[qd];
                     }
                     const uint32_t sr = PACK ? (wrb & 0xffffu) : wrb;
                     const uint32_t sb = PACK ? (wrb >> 16) : wb;
                     c0f[i] = (float)(ctr[i] & 0xffu);
                     c1f[i] = (float)((ctr[i] >> 8) & 0xffu);
                     c2f[i] = (float)((ctr[i] >> 16) & 0xffu);
+                    // opaque to the optimiser: otherwise fsub(uitofp n, uitofp c) in the tap
+                    // loop is rewritten as an integer v_sub_u32_sdwa + v_cvt_f32_i32 per
+                    // channel and pair (two slow ops instead of one v_sub_f32)
+                    __asm__("" : "+v"(c0f[i]), "+v"(c1f[i]), "+v"(c2f[i]));
                     o0[i] = c0f[i] - (float)sr / kk;
                     o1[i] = c1f[i] - (float)wg / kk;
                     o2[i] = c2f[i] - (float)sb / kk;
@@ -109,19 +141,19 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
             }
 
             // ---- pass 2: offset-weighted bilateral over the disc ----
-            f2 a01[kP], a2k[kP];  // {sum_b, sum_g}, {sum_r, sumk}
+            f2 a01[P], a2k[P];  // {sum_b, sum_g}, {sum_r, sumk}
         #pragma unroll
-        for (int i = 0; i < kP; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
+            for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
             for (int ky = -R; ky <= R; ++ky) {
                 const int aky = ky < 0 ? -ky : ky;
                 const int hw = circle_hw(R, aky);
                 set_progress_priority((ky + R) * 4 / (2 * R + 1));
-                const int row_off = (ty + R + ky) * G::S + tx * kP;
+                const int row_off = (ty + R + ky) * G::S + tx * P;
                 const float* const ws = a.ws + aky * kWsStride;
                 HwDispatch<R, 0>::run(hw, [&](auto hwc) {
                     constexpr int HW = decltype(hwc)::value;
-                    constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
+                    constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + P - 1 + HW) / 4;
                     constexpr int NC = C1 - C0 + 1;
                     uint32_t gp[4 * NC];
                     load_row<C0, NC>(plane, row_off, gp);
@@ -130,20 +162,21 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
                     // dist = |(n0-c0)-o0| + |(n1-c1)-o1| + |(n2-c2)-o2|; (float)(n-c) == f_n - f_c exactly.
                     // Index int(dist) <= 1530 -> word d*16 + (lane & 15) of the 1536 x 16 LUT.
-                    auto widx = [&](uint32_t, float f0, float f1, float f2, int i) {
-                        const float d0 = (f0 - c0f[i]) - o0[i];
-                        const float d1 = (f1 - c1f[i]) - o1[i];
-                        const float d2 = (f2 - c2f[i]) - o2[i];
+                    auto widx = [&](uint32_t, f2 n01, f2 n21, int i) {
+                        // {b, g} channels as v_pk_add_f32 pairs (each half an IEEE subtract)
+                        const f2 d01 = (n01 - f2{c0f[i], c1f[i]}) - f2{o0[i], o1[i]};
+                        const float d0 = d01.x, d1 = d01.y;
+                        const float d2 = (n21.x - c2f[i]) - o2[i];
                         const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
                         return ((uint32_t)dist << 6) | lane16;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA, true>(gp, gp, wsv, lut_bytes, widx, a01, a2k);
+                    row_taps<HW, G::L, C0, 4 * NC, FMA, true, P>(gp, gp, wsv, lut_bytes, widx, a01, a2k);
                 });
             }
 
-            uint32_t o[kP];
-        finish_outputs(a01, a2k, o);
-            store8(a, ty0 + ty, tx0 + tx * kP, o);
+            uint32_t o[P];
+            finish_outputs(a01, a2k, o);
+            store_px(a, ty0 + ty, tx0 + tx * P, o);
         }
         if (next >= a.tiles_total) break;
         __syncthreads();
@@ -155,13 +188,15 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
 
 template <int R, bool FMA>
 static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
-    // 8 waves: the per-output centre/offset floats (48 VGPRs) plus the pipelined
-    // LUT reads need more than the 128 VGPRs a 16-wave workgroup allows
-    constexpr int WAVES = pick_waves<R, 1, 8>();
+    // P = 8 outputs per thread needs ~170 VGPRs (per-output centre/offset floats,
+    // accumulators, pipelined LUT reads) -> 8 waves; P = 4 fits 128 -> 16 waves
+    constexpr int P = VIP_ADA_P;
+    using G = Geom<R, P>;
+    constexpr int WAVES = pick_waves<R, 1, P == 8 ? 8 : 16, lut_words(true), P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, 1>();
-    auto kern = adaptive_kernel<R, WAVES, FMA>;
+    constexpr int LDS = lds_bytes<R, WAVES, 1, lut_words(true), P>();
+    auto kern = adaptive_kernel<R, WAVES, FMA, P>;
     static bool attr_done = false;
     if (!attr_done) {
         VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -169,7 +204,8 @@ static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
         attr_done = true;
     }
     StencilArgs args = a;
-    args.tiles_total = a.tiles_x * ((a.out_rows + TH - 1) / TH);
+    args.tiles_x = (a.width + G::TW - 1) / G::TW;
+    args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
@@ -182,7 +218,7 @@ static int launch_adaptive_dispatch(int radius, const StencilArgs& a, hipStream_
 #define VIP_CASE(RR) \
     case RR: return launch_adaptive_r<RR, FMA>(a, stream);
 #ifdef VIP_ONLY_R7
-        VIP_CASE(7)
+        VIP_CASE(4) VIP_CASE(7)
 #else
         VIP_CASE(1) VIP_CASE(2) VIP_CASE(3) VIP_CASE(4) VIP_CASE(5) VIP_CASE(6) VIP_CASE(7) VIP_CASE(8)
         VIP_CASE(9) VIP_CASE(10) VIP_CASE(11) VIP_CASE(12) VIP_CASE(13) VIP_CASE(14) VIP_CASE(15)

@@ -30,7 +30,7 @@ __device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
 #define VIP_STAMP(t, k)
 #endif
 
-template <int R, int WAVES, bool JOINT, bool FMA>
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R>;
     constexpr int NT = WAVES * 64;
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     constexpr int PLANE = ROWS * G::S;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
-    uint32_t* const gplane = lds + lut_words(false);
+    uint32_t* const gplane = lds + 768 * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
     const int tid = threadIdx.x;
@@ -47,28 +47,31 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = lane & 15;
     const int ty = wave * 4 + (lane >> 4);
-    const uint32_t lane4 = (uint32_t)(lane & 31) << 2;
+    const uint32_t lane4 = (uint32_t)(lane & (COPIES - 1)) << 2;  // this lane's LUT copy
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
     int tile = blockIdx.x;
     TilePrefetch<R, ROWS, NT> pg, ps;
     {
-        const int tx0 = (tile % a.tiles_x) * kTW, ty0 = (tile / a.tiles_x) * TH;
+        const int mt = xcd_tile(tile, a.tiles_total);
+        const int tx0 = (mt % a.tiles_x) * kTW, ty0 = (mt / a.tiles_x) * TH;
         pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
-    stage_lut<NT, 768>(lut, a.color);  // once per workgroup
+    stage_lut<NT, 768, COPIES>(lut, a.color);  // once per workgroup
     pg.commit(gplane);
     if constexpr (JOINT) ps.commit(splane);
     __syncthreads();
 
-    for (int it = 0;; ++it) {
+    for ([[maybe_unused]] int it = 0;; ++it) {
         VIP_STAMP(it, 0);
-        const int tx0 = (tile % a.tiles_x) * kTW, ty0 = (tile / a.tiles_x) * TH;
+        const int mt = xcd_tile(tile, a.tiles_total);
+        const int tx0 = (mt % a.tiles_x) * kTW, ty0 = (mt / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
         if (next < a.tiles_total) {  // next tile's HBM reads fly under this tile's taps
-            const int nx0 = (next % a.tiles_x) * kTW, ny0 = (next / a.tiles_x) * TH;
+            const int mn = xcd_tile(next, a.tiles_total);
+            const int nx0 = (mn % a.tiles_x) * kTW, ny0 = (mn / a.tiles_x) * TH;
             pg.issue(a.guide, a.guide_pitch, a, nx0, ny0);
             if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
         }
@@ -106,17 +109,17 @@ for (int i = 0; i < kP; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
                     float wsv[HW + 1];
 #pragma unroll
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
-                    // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*32 + (lane & 31)
-                    auto widx = [&](uint32_t g, float, float, float, int i) {
-                        return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << 7) | lane4;
+                    // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*COPIES + lane copy
+                    auto widx = [&](uint32_t g, f2, f2, int i) {
+                        return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << (COPIES == 32 ? 7 : 6)) | lane4;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA, false>(gp, sp, wsv, lut_bytes, widx, a01, a2k);
+                    row_taps<HW, G::L, C0, 4 * NC, FMA, false, kP>(gp, sp, wsv, lut_bytes, widx, a01, a2k);
                 });
             }
 
             uint32_t o[kP];
 finish_outputs(a01, a2k, o);
-            store8(a, ty0 + ty, tx0 + tx * kP, o);
+            store_px(a, ty0 + ty, tx0 + tx * kP, o);
         }
         VIP_STAMP(it, 1);
         if (next >= a.tiles_total) break;
@@ -129,14 +132,27 @@ finish_outputs(a01, a2k, o);
     }
 }
 
+// The joint kernel holds two tile planes; when the full 32-copy LUT leaves room for
+// fewer than 16 waves, a 16-copy LUT (lanes l and l+16 of a half-wave share a copy:
+// at most 2-way bank conflicts) is used if it buys more waves (VIP_JBF_LUT16=0 disables).
+#ifndef VIP_JBF_LUT16
+#define VIP_JBF_LUT16 1
+#endif
+template <int R, int PLANES>
+constexpr int lut_copies() {
+    if (!VIP_JBF_LUT16 || PLANES == 1) return 32;
+    return pick_waves<R, PLANES, 16, 768 * 16>() > pick_waves<R, PLANES>() ? 16 : 32;
+}
+
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
-    constexpr int WAVES = pick_waves<R, PLANES>();
+    constexpr int COPIES = lut_copies<R, PLANES>();
+    constexpr int WAVES = pick_waves<R, PLANES, 16, 768 * COPIES>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, PLANES>();
-    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA>;
+    constexpr int LDS = lds_bytes<R, WAVES, PLANES, 768 * COPIES>();
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES>;
     static bool attr_done = false;  // benign race: idempotent attribute set
     if (!attr_done) {
         VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -157,7 +173,7 @@ static int launch_bilateral_dispatch(int radius, const StencilArgs& a, hipStream
 #define VIP_CASE(RR) \
     case RR: return launch_bilateral_r<RR, JOINT, FMA>(a, stream);
 #ifdef VIP_ONLY_R7
-        VIP_CASE(7)
+        VIP_CASE(4) VIP_CASE(7)
 #else
         VIP_CASE(1) VIP_CASE(2) VIP_CASE(3) VIP_CASE(4) VIP_CASE(5) VIP_CASE(6) VIP_CASE(7) VIP_CASE(8)
         VIP_CASE(9) VIP_CASE(10) VIP_CASE(11) VIP_CASE(12) VIP_CASE(13) VIP_CASE(14) VIP_CASE(15)

@@ -55,28 +55,50 @@ inline int persistent_blocks(int tiles) {
 
 constexpr int lut_words(bool adaptive) { return adaptive ? 1536 * 16 : 768 * 32; }
 
-template <int R>
+// Tile filtered by a persistent workgroup at `slot` (= blockIdx.x + k * gridDim.x, round
+// k). In full rounds each XCD (workgroups are dispatched round-robin over the 8 XCDs,
+// b % 8) gets a run of gridDim.x / 8 consecutive row-major tiles, so horizontally
+// adjacent tiles, whose aprons share cache lines, meet in the same L2. The last,
+// partial round keeps the identity map. Placement affects speed only, never results.
+__device__ __forceinline__ int xcd_tile(int slot, int total) {
+    const int grid = (int)gridDim.x, b = (int)blockIdx.x;
+    const int base = slot - b;
+#ifdef VIP_NO_XCD_MAP
+    return slot;
+#endif
+    if ((grid & 7) != 0 || base + grid > total) return slot;
+    return base + (b & 7) * (grid >> 3) + (b >> 3);
+}
+
+// P outputs per thread (8, or 4 for register-heavy kernels), 16 threads per tile row.
+// S makes the ds_read_b128 row loads conflict-free: with P = 8 the 16 lanes of a
+// b128 group read words tx*8 + 4c of rows ty, ty+1 -> S = 4 (mod 8); with P = 4
+// they read 64 contiguous words per row -> S = 0 (mod 64).
+template <int R, int P = kP>
 struct Geom {
-    static constexpr int L = round_up(R, 4);               // left/right apron, 4-px aligned
-    static constexpr int S = round_up(kTW + 2 * L, 8) + 4;  // LDS row stride (words)
-    static constexpr int GROUPS = (kTW + 2 * L) / 4;        // 4-pixel groups per tile row
+    static_assert(P == 8 || P == 4, "P");
+    static constexpr int TW = 16 * P;                        // tile width in pixels
+    static constexpr int L = round_up(R, 4);                 // left/right apron, 4-px aligned
+    static constexpr int S = P == 8 ? round_up(TW + 2 * L, 8) + 4 : round_up(TW + 2 * L, 64);
+    static constexpr int GROUPS = (TW + 2 * L) / 4;          // 4-pixel groups per tile row
 };
 
-// Largest wave count (<= MAXW: 16, 12, 8 or 4) whose LUT + plane(s) fit the CU's LDS.
-template <int R, int PLANES, int MAXW = 16>
+// Largest wave count (<= MAXW: 16, 12, 8 or 4) whose LUT (LUTW words) + plane(s) fit
+// the CU's LDS.
+template <int R, int PLANES, int MAXW = 16, int LUTW = lut_words(false), int P = kP>
 constexpr int pick_waves() {
     constexpr int cand[4] = {16, 12, 8, 4};
     for (int w : cand) {
         if (w > MAXW) continue;
-        const long long bytes = 4LL * lut_words(false) + 4LL * PLANES * (w * 4 + 2 * R) * Geom<R>::S;
+        const long long bytes = 4LL * LUTW + 4LL * PLANES * (w * 4 + 2 * R) * Geom<R, P>::S;
         if (bytes <= kLdsBudget) return w;
     }
     return 0;
 }
 
-template <int R, int WAVES, int PLANES>
+template <int R, int WAVES, int PLANES, int LUTW = lut_words(false), int P = kP>
 constexpr int lds_bytes() {
-    return 4 * lut_words(false) + 4 * PLANES * (WAVES * 4 + 2 * R) * Geom<R>::S;
+    return 4 * LUTW + 4 * PLANES * (WAVES * 4 + 2 * R) * Geom<R, P>::S;
 }
 
 // Calls f(std::integral_constant<int, HW>) for the runtime circle half-width hw.
@@ -120,9 +142,9 @@ __device__ __forceinline__ uint32_t load_rgb(const uint8_t* row, int x) {
 // byte loads otherwise) and returns at once; commit() unpacks RGB to RGBX words
 // and writes the LDS plane. A persistent workgroup issues tile t+1 before it
 // computes tile t, so HBM latency hides under the VALU-bound tap loop.
-template <int R, int ROWS, int NT>
+template <int R, int ROWS, int NT, int P = kP>
 struct TilePrefetch {
-    using G = Geom<R>;
+    using G = Geom<R, P>;
     static constexpr int NG = ROWS * G::GROUPS;
     static constexpr int K = (NG + NT - 1) / NT;
     uint32_t raw[K][3];
@@ -168,12 +190,13 @@ struct TilePrefetch {
 };
 
 // Fill the interleaved colour LUT: word d*COPIES + c = color[d], for
-// 768 entries x 32 copies (bilateral) or 1536 x 16 (adaptive) = 96 KiB.
-template <int NT, int ENTRIES>
+// 768 entries x 32 copies (bilateral, 96 KiB), 768 x 16 (joint bilateral when the
+// halved LUT buys more waves, 48 KiB) or 1536 x 16 (adaptive, 96 KiB).
+template <int NT, int ENTRIES, int COPIES>
 __device__ __forceinline__ void stage_lut(uint32_t* lut, const float* color) {
-    constexpr int COPIES = 768 * 32 / ENTRIES;
-    constexpr int SHIFT = COPIES == 32 ? 3 : 2;  // (4 words per store) / COPIES
-    for (int q = threadIdx.x; q < 768 * 32 / 4; q += NT) {
+    static_assert(COPIES == 16 || COPIES == 32, "copies");
+    constexpr int SHIFT = COPIES == 32 ? 3 : 2;  // log2(COPIES / 4 words per store)
+    for (int q = threadIdx.x; q < ENTRIES * COPIES / 4; q += NT) {
         const uint32_t v = __float_as_uint(color[q >> SHIFT]);
         *reinterpret_cast<uint4*>(lut + 4 * q) = make_uint4(v, v, v, v);
     }
@@ -225,23 +248,23 @@ __device__ __forceinline__ void set_progress_priority(int band) {
 // VIP_PIPE_DEPTH neighbour columns ahead: while column j's weights are
 // accumulated, the colour-LUT reads of columns j+1..j+D are already in flight
 // (the LDS latency is hidden inside the wave, not only across waves).
-// `widx(g, f0, f1, f2, i)` returns the LDS byte address of the colour weight of
-// guide word g (source floats f*) for output i. Accumulation order per output is
+// `widx(g, n01, n21, i)` returns the LDS byte address of the colour weight of
+// guide word g (source floats {b, g}, {r, 1}) for output i. Accumulation order per output is
 // ascending kx, as in the reference's row-major loop.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
 // PK: accumulate with v_pk_fma_f32 ({s0,s1} and {s2,sk} pairs). Measured on gfx950:
 // +3 % for the adaptive kernel, -10 % for the bilateral kernel (the {r, 1} pairs
 // push it past 128 VGPRs), so it is a per-kernel choice.
-template <int HW, int L, int C0, int NGP, bool FMA, bool PK, class WIdx>
+template <int HW, int L, int C0, int NGP, bool FMA, bool PK, int P, class WIdx>
 __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32_t (&sp)[NGP],
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
-                                         f2 (&a01)[kP], f2 (&a2k)[kP]) {
+                                         f2 (&a01)[P], f2 (&a2k)[P]) {
     constexpr int D = VIP_PIPE_DEPTH;
     constexpr int NB = D + 1;            // ring of in-flight columns
-    constexpr int J0 = L - HW;           // first neighbour column relative to the thread's 8
-    constexpr int J1 = L + kP - 1 + HW;  // last
-    float wc[NB][kP];
+    constexpr int J0 = L - HW;           // first neighbour column relative to the thread's P
+    constexpr int J1 = L + P - 1 + HW;   // last
+    float wc[NB][P];
     f2 n01[NB], n21[NB];                 // {b, g} and {r, 1} of the neighbour (source image)
     auto issue = [&](int j) {
         const uint32_t g = gp[j - 4 * C0];
@@ -252,10 +275,10 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
         n21[b].x = (float)((p >> 16) & 0xffu);
         n21[b].y = 1.0f;
 #pragma unroll
-        for (int i = 0; i < kP; ++i) {
+        for (int i = 0; i < P; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b].x, n01[b].y, n21[b].x, i));
+            wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b], n21[b], i));
         }
     };
 #pragma unroll
@@ -265,7 +288,7 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
         if (j + D <= J1) issue(j + D);
         const int b = (j - J0) % NB;
 #pragma unroll
-        for (int i = 0; i < kP; ++i) {
+        for (int i = 0; i < P; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
             const float w = wc[b][i] * wsv[kx < 0 ? -kx : kx];
@@ -293,20 +316,30 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
     }
 }
 
-// dst = u8(sum_c / sumk + 0.5f) for the kP outputs, packed as RGBX words
-__device__ __forceinline__ void finish_outputs(const f2 (&a01)[kP], const f2 (&a2k)[kP], uint32_t (&o)[kP]) {
+// dst = u8(sum_c / sumk + 0.5f) for the P outputs, packed as RGBX words
+template <int P>
+__device__ __forceinline__ void finish_outputs(const f2 (&a01)[P], const f2 (&a2k)[P], uint32_t (&o)[P]) {
 #pragma unroll
-    for (int i = 0; i < kP; ++i) {
+    for (int i = 0; i < P; ++i) {
         const float sk = a2k[i].y;
         o[i] = f2u8(a01[i].x / sk + 0.5f) | (f2u8(a01[i].y / sk + 0.5f) << 8) | (f2u8(a2k[i].x / sk + 0.5f) << 16);
     }
 }
 
-// Write 8 RGB outputs (24 bytes) of row oy starting at column x.
-__device__ __forceinline__ void store8(const StencilArgs& a, int oy, int x, const uint32_t (&o)[kP]) {
+// Write P RGB outputs (3P bytes) of row oy starting at column x.
+template <int P>
+__device__ __forceinline__ void store_px(const StencilArgs& a, int oy, int x, const uint32_t (&o)[P]) {
     if (oy >= a.out_rows || x >= a.width) return;
     uint8_t* row = a.dst + (long long)oy * a.dst_pitch;
-    if (a.dst_aligned && x + kP <= a.width) {
+    if constexpr (P == 4) {
+        if (a.dst_aligned && x + P <= a.width) {  // 12 bytes at a 4-byte aligned address
+            uint32_t* p = reinterpret_cast<uint32_t*>(row + 3 * x);
+            p[0] = o[0] | (o[1] << 24);
+            p[1] = (o[1] >> 8) | (o[2] << 16);
+            p[2] = (o[2] >> 16) | (o[3] << 8);
+            return;
+        }
+    } else if (a.dst_aligned && x + P <= a.width) {
         uint32_t w[6];
         w[0] = o[0] | (o[1] << 24);
         w[1] = (o[1] >> 8) | (o[2] << 16);
@@ -318,9 +351,11 @@ __device__ __forceinline__ void store8(const StencilArgs& a, int oy, int x, cons
         p[0] = make_uint2(w[0], w[1]);
         p[1] = make_uint2(w[2], w[3]);
         p[2] = make_uint2(w[4], w[5]);
-    } else {
+        return;
+    }
+    {
 #pragma unroll
-        for (int i = 0; i < kP; ++i) {
+        for (int i = 0; i < P; ++i) {
             if (x + i < a.width) {
                 uint8_t* p = row + 3 * (x + i);
                 p[0] = (uint8_t)(o[i]);
