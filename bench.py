@@ -99,6 +99,26 @@ def cpu_baseline(cfg) -> dict:
                        f"(oracle CPP profile = include/cpp numerics, all k*k taps like the reference loop)")
 
 
+def pmc_traffic(config: str, kernels: list, per_step: int = 1):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this config
+    (profiles/r*_<config>_pmc.json, written by scripts/pmc_summary.py from
+    scripts/gpu_pmc.sh: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE).
+    Returns (bytes, source) or (None, None) when no summary matches the kernels."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        ks = json.load(fh)["kernels"]
+    total = 0.0
+    for want in kernels:
+        hit = [v for n, v in ks.items() if n.startswith(want) and "traffic_bytes" in v]
+        if not hit:
+            return None, None
+        total += hit[0]["traffic_bytes"]
+    return total * per_step, os.path.relpath(files[-1], ROOT)
+
+
 def main():
     args = parse()
     import torch
@@ -146,19 +166,27 @@ def main():
         srcs = [torch.randint(0, 255, (geo.slab_rows, w, 3), dtype=torch.uint8, device=dev, generator=gen)
                 for _ in range(NBUF)]
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
+        # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time.
+        # N>1: the halo exchange sits between kernels, so every KSAMPLE-th kernel is
+        # bracketed by its own events (an event pair costs ~11 us of stream time,
+        # measured with rocprofv3, so not every step carries one).
+        KSAMPLE = 4
         kstart = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
         kend = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        timed = {"on": False, "i": 0}
+        timed = {"on": False, "i": 0, "n": 0}
 
         def step(i):
             from various_image_processings_amd.sharded import exchange_halo
             if world > 1:
                 exchange_halo(srcs[i % NBUF], geo)
-            if timed["on"]:
-                kstart[timed["i"]].record(stream)
+            sample = timed["on"] and world > 1 and timed["i"] % KSAMPLE == 0
+            if sample:
+                kstart[timed["n"]].record(stream)
             sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
+            if sample:
+                kend[timed["n"]].record(stream)
+                timed["n"] += 1
             if timed["on"]:
-                kend[timed["i"]].record(stream)
                 timed["i"] += 1
 
     for i in range(args.warmup):
@@ -180,8 +208,9 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if cfg["kind"] != "texture":
-        kernel_ms = sum(a.elapsed_time(b) for a, b in zip(kstart, kend)) / args.steps
+    if cfg["kind"] != "texture" and timed["n"] > 0:
+        n = timed["n"]
+        kernel_ms = sum(a.elapsed_time(b) for a, b in zip(kstart[:n], kend[:n])) / n
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
     t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
@@ -199,8 +228,10 @@ def main():
         # blur_rtv 7+16, guide 16+3, JBF 6+3 = 58 B
         bytes_launch = 58.0 * px_per_rank * cfg["nitr"]
         achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(args.config, ["void vip::texture_guide_fused_kernel", "void vip::bilateral_kernel"],
+                                    cfg["nitr"])
         roof = dict(bound="hbm", achieved=round(achieved, 2), peak=PEAK_HBM_GBS, unit="GB/s",
-                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=None,
+                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=traffic, traffic_source=tsrc,
                     kernel="whole texture pipeline per launch (gradient, blur_rtv, guide, JBF) x nitr",
                     avg_launch_ms=round(kernel_ms, 4))
     else:
@@ -208,8 +239,11 @@ def main():
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
         tflops = flops / (kernel_ms * 1e-3) / 1e12
         hbm = 6.0 * px_per_rank / (kernel_ms * 1e-3) / 1e9
+        traffic, tsrc = (None, None) if world > 1 or "frame_height" in cfg else \
+            pmc_traffic(args.config, [f"void vip::{cfg['kind']}_kernel<{r},"])
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
-                    frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=None,
+                    frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
+                    traffic_algorithmic=6.0 * px_per_rank,
                     kernel=f"{cfg['kind']}_kernel<R={r}>", avg_launch_ms=round(kernel_ms, 4),
                     flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
@@ -226,8 +260,8 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if "frame_height" in cfg else "weak",
         "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic uniform u8 (torch.randint 0..254), resident in HBM",
+        "dtype": "f32",
+        "data": "synthetic uniform u8 RGB (torch.randint 0..254), resident in HBM; f32 weights/sums",
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows,
                    "parallelism": f"row-tiled x{world}" + (" + r-row halo sendrecv" if world > 1 and geo else "")},

@@ -7,6 +7,8 @@
 
 template <int KIND>
 __global__ __launch_bounds__(1024) void k(float* out, float a, float b) {
+    __shared__ unsigned sh[16384];  // 64 KiB for the ds_read mix
+    if (KIND == 40 && a < -1e30f) sh[threadIdx.x] = 1u;
     float x[8];
     for (int i = 0; i < 8; ++i) x[i] = threadIdx.x * 0.001f + i;
     unsigned u[8];
@@ -131,6 +133,30 @@ __global__ __launch_bounds__(1024) void k(float* out, float a, float b) {
                 if (i & 1) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
                 else asm volatile("v_cvt_f32_ubyte1 %0, %1" : "=v"(x[i]) : "v"(u[i]));
             }
+            if constexpr (KIND == 36) {  // pk_fma / sad 1:1
+                if (i & 1) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+                else asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[0]), "v"(*(double*)&x[2]));
+            }
+            if constexpr (KIND == 37) {  // pk_fma / fma 1:1
+                if (i & 1) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+                else asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[0]), "v"(*(double*)&x[2]));
+            }
+            if constexpr (KIND == 38) {  // sad, lshl_or, pk_fma, pk_fma x2
+                switch (i & 3) {
+                    case 0: asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7])); break;
+                    case 1: asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(u[i]) : "v"(u[(i + 1) & 7])); break;
+                    default: asm volatile("v_pk_fma_f32 %0, %1, %2, %0" : "+v"(*reinterpret_cast<double*>(&x[(i & 1) * 2 + 4])) : "v"(*(double*)&x[0]), "v"(*(double*)&x[2])); break;
+                }
+            }
+            if constexpr (KIND == 39) {  // pk_mul / mul 1:1 and pk_add
+                if (i & 1) asm volatile("v_mul_f32 %0, %1, %0" : "+v"(x[i]) : "v"(a));
+                else asm volatile("v_pk_mul_f32 %0, %1, %0" : "+v"(*reinterpret_cast<double*>(&x[i & ~1])) : "v"(*(double*)&x[2]));
+            }
+            if constexpr (KIND == 40) {  // ds_read_b32 + fma 1:3 (LDS issue alongside VALU)
+                if ((i & 3) == 0) { asm volatile("ds_read_b32 %0, %1" : "=v"(u[i]) : "v"(u[(i+1)&7] & 0xfffcu)); }
+                else asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+                if (i == 7) asm volatile("s_waitcnt lgkmcnt(0)");
+            }
             if constexpr (KIND == 35) {  // 1 slow : 3 fast
                 if ((i & 3) == 0) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
                 else asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
@@ -198,5 +224,10 @@ int main() {
     run<33>("mix bilateral pair 8", d, blocks, 0);
     run<34>("mix cvt/sad 1:1", d, blocks, 0);
     run<35>("mix sad/fma 1:3", d, blocks, 0);
+    run<36>("mix pk_fma/sad 1:1", d, blocks, 0);
+    run<37>("mix pk_fma/fma 1:1", d, blocks, 0);
+    run<38>("mix sad,lshl_or,2 pk_fma", d, blocks, 0);
+    run<39>("mix pk_mul/mul 1:1", d, blocks, 0);
+    run<40>("mix ds_read/fma 1:3", d, blocks, 0);
     return 0;
 }

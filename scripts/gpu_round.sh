@@ -16,3 +16,9 @@ rc=$?; echo "sample rc=$rc"; cat gpurun_out/sample.log | tail -6; [ $rc -eq 0 ] 
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c2 -o run --output-format csv -- python bench.py --steps 10 --no-cpu-baseline > gpurun_out/prof_c2.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; find gpurun_out/prof_c2 -name "*stats*" | head
+[ $rc -eq 0 ] || exit $rc
+for cfg in c3 c4 c5; do
+  timeout -k 10 400 python bench.py --config $cfg --steps 10 --warmup 2 > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err
+  rc=$?; echo "bench $cfg rc=$rc"; cut -c1-400 gpurun_out/bench_$cfg.json; [ $rc -eq 0 ] || exit $rc
+done
+for cfg in c3 c4; do bash scripts/gpu_prof_cfg.sh $cfg || exit $?; done

@@ -138,17 +138,22 @@ finish_outputs(a01, a2k, o);
 #ifndef VIP_JBF_LUT16
 #define VIP_JBF_LUT16 1
 #endif
+#ifndef VIP_JBF_MAXW
+#define VIP_JBF_MAXW 16
+#endif
 template <int R, int PLANES>
 constexpr int lut_copies() {
     if (!VIP_JBF_LUT16 || PLANES == 1) return 32;
-    return pick_waves<R, PLANES, 16, 768 * 16>() > pick_waves<R, PLANES>() ? 16 : 32;
+    return pick_waves<R, PLANES, VIP_JBF_MAXW, 768 * 16>() > pick_waves<R, PLANES>() ? 16 : 32;
 }
+template <int R, int PLANES>
+constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
 
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
     constexpr int COPIES = lut_copies<R, PLANES>();
-    constexpr int WAVES = pick_waves<R, PLANES, 16, 768 * COPIES>();
+    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), 768 * COPIES>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
     constexpr int LDS = lds_bytes<R, WAVES, PLANES, 768 * COPIES>();
