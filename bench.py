@@ -13,8 +13,9 @@ the ranks exchange their r-row halos (sendrecv with the row neighbours only).
      owns a full 3840x2160 RGB8 frame's worth of rows of an (N*2160)x3840 frame
      -> weak scaling; at N=1 this is exactly BASELINE config 2.
   c3 adaptive bilateral r=7, same geometry (BASELINE config 3).
-  c4 bilateral texture filter k=5, nitr=5 on 3840x2160 per rank, no halo
-     (independent frames; BASELINE config 4).
+  c4 bilateral texture filter k=5, nitr=5 on 3840x2160 per rank (BASELINE config
+     4); N>1 row-shards an (N*2160)x3840 frame with one 45-row halo exchange per
+     frame (sharded.ShardedTexture).
   c5 bilateral r=15 (ksize 31) on ONE 16384x16384 frame row-tiled over the N
      GPUs (strong scaling; BASELINE config 5).
 
@@ -69,6 +70,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    # rehearsal only: gloo + every rank on cuda:0 runs the N>1 code path on a 1-GPU box
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    p.add_argument("--same-device", action="store_true")
     return p.parse_args()
 
 
@@ -131,15 +135,20 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         dist.barrier()  # communicator up before the first (P2P) halo exchange
 
     import various_image_processings_amd as vip
     from various_image_processings_amd.filters import _TextureImpl
-    from various_image_processings_amd.sharded import ShardedBilateral, SlabGeometry
+    from various_image_processings_amd.sharded import ShardedBilateral
 
     stream = torch.cuda.current_stream(dev)
     w = cfg["width"]
@@ -148,9 +157,9 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
 
-    if cfg["kind"] == "texture":
+    if cfg["kind"] == "texture" and world == 1:
         rows = cfg["rows_per_rank"]
-        frame_h = rows * world
+        frame_h = rows
         geo = None
         tex = _TextureImpl(w, rows, k, cfg["nitr"])
         srcs = [torch.randint(0, 255, (rows, w, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(NBUF)]
@@ -158,6 +167,21 @@ def main():
 
         def step(i):
             tex.execute(srcs[i % NBUF], dsts[i % NBUF], stream=stream)
+    elif cfg["kind"] == "texture":
+        # row-sharded frame: one halo exchange of nitr * texture_halo_rows(k) rows per
+        # frame, then shrinking ghost zones (sharded.ShardedTexture)
+        from various_image_processings_amd.sharded import ShardedTexture, exchange_halo
+        frame_h = cfg["rows_per_rank"] * world
+        st = ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world)
+        geo = st.geo
+        rows = geo.own
+        srcs = [torch.randint(0, 255, (geo.slab_rows, w, 3), dtype=torch.uint8, device=dev, generator=gen)
+                for _ in range(NBUF)]
+        dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
+
+        def step(i):
+            exchange_halo(srcs[i % NBUF], geo)
+            st.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
     else:
         frame_h = cfg.get("frame_height", cfg.get("rows_per_rank", 0) * world)
         sb = ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
@@ -213,7 +237,7 @@ def main():
         kernel_ms = sum(a.elapsed_time(b) for a, b in zip(kstart[:n], kend[:n])) / n
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms = float(t[0]), float(t[1])
@@ -264,7 +288,8 @@ def main():
         "data": "synthetic uniform u8 RGB (torch.randint 0..254), resident in HBM; f32 weights/sums",
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows,
-                   "parallelism": f"row-tiled x{world}" + (" + r-row halo sendrecv" if world > 1 and geo else "")},
+                   "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
+                   **({"backend": args.backend} if world > 1 else {})},
         "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -13,6 +13,8 @@ public:
     ~CudaAdaptiveBilateralFilter();
 
     void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst) const;
+    // additive non-blocking overload: enqueue on `stream` (hipStream_t as void*)
+    void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream) const;
 
 protected:
     class Impl;  // adaptive_bilateral_filter_impl.cuh

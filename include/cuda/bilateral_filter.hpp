@@ -21,6 +21,12 @@ public:
     void joint_bilateral_filter(const std::uint8_t* const d_src, const std::uint8_t* const d_guide,
                                 std::uint8_t* const d_dst) const;
 
+    // Additive, non-blocking overloads: enqueue on `stream` (a
+    // hipStream_t passed as void*, nullptr = default stream) and return at once.
+    void bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream) const;
+    void joint_bilateral_filter(const std::uint8_t* const d_src, const std::uint8_t* const d_guide,
+                                std::uint8_t* const d_dst, void* stream) const;
+
 protected:
     class Impl;  // defined in bilateral_filter_impl.cuh (test drivers reach it through impl_)
     std::unique_ptr<Impl> impl_;

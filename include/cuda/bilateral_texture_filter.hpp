@@ -13,6 +13,8 @@ public:
     ~CudaBilateralTextureFilter();
 
     void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst);
+    // additive non-blocking overload: enqueue on `stream` (hipStream_t as void*)
+    void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream);
 
 protected:
     class Impl;  // bilateral_texture_filter_impl.cuh

@@ -13,10 +13,18 @@ public:
     ~DeviceImage();
     DeviceImage(const DeviceImage&) = delete;
     DeviceImage& operator=(const DeviceImage&) = delete;
+    DeviceImage(DeviceImage&& other) noexcept;
+    DeviceImage& operator=(DeviceImage&& other) noexcept;
 
     void upload(const ElemType* const data);
     void download(ElemType* const data);
     ElemType* get();
+
+    // Additive stream-ordered copies. `stream` is a hipStream_t
+    // passed as void*; the host buffer should be page-locked (vip_host_alloc) for
+    // the copy to overlap with kernels on other streams.
+    void upload_async(const ElemType* const data, void* stream);
+    void download_async(ElemType* const data, void* stream);
 
 private:
     class Impl;

@@ -17,6 +17,7 @@ public:
     Impl& operator=(const Impl&) = delete;
 
     void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst) const;
+    void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream) const;
 
     vip_adaptive_t handle() const { return handle_; }
 

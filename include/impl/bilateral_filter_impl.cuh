@@ -21,6 +21,9 @@ public:
     void bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst) const;
     void joint_bilateral_filter(const std::uint8_t* const d_src, const std::uint8_t* const d_guide,
                                 std::uint8_t* const d_dst) const;
+    void bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream) const;
+    void joint_bilateral_filter(const std::uint8_t* const d_src, const std::uint8_t* const d_guide,
+                                std::uint8_t* const d_dst, void* stream) const;
 
     vip_bilateral_t handle() const { return handle_; }
 

@@ -26,6 +26,7 @@ public:
     Impl& operator=(const Impl&) = delete;
 
     void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst);
+    void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream);
 
     // stage entry points (no synchronisation), raw device pointers
     void compute_blur_and_rtv(const std::uint8_t* d_image, const float* d_magnitude, float* d_blurred, float* d_rtv);

@@ -53,6 +53,17 @@ int vip_download(void* h_dst, const void* d_src, size_t bytes); /* blocking D2H 
 int vip_device_synchronize(void);
 int vip_stream_synchronize(void* stream);
 
+/* ---- host-frame path (the reference's DeviceImage::upload/download,
+ *      src/device_image.cu:10-16, copy pageable memory synchronously through thrust).
+ *      Pinned host frames + stream-ordered copies let H2D, kernels and D2H of
+ *      successive frames overlap on separate streams. ---- */
+int vip_host_alloc(void** h_ptr, size_t bytes);  /* page-locked host memory */
+int vip_host_free(void* h_ptr);
+int vip_upload_async(void* d_dst, const void* h_src, size_t bytes, void* stream);   /* stream-ordered H2D */
+int vip_download_async(void* h_dst, const void* d_src, size_t bytes, void* stream); /* stream-ordered D2H */
+int vip_stream_create(void** stream);  /* non-blocking HIP stream, returned as void* */
+int vip_stream_destroy(void* stream);
+
 /* ---- bilateral / joint bilateral: CudaBilateralFilter
  *      (include/cuda/bilateral_filter.hpp:9-24, src/bilateral_filter_impl.cu:204-310) ---- */
 int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space,
@@ -96,6 +107,17 @@ int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int
 int vip_texture_destroy(vip_texture_t h);
 /* Impl::execute (:199-214); d_src and d_dst are dense width*3 */
 int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream);
+
+/* Row-slab form of one texture iteration for a row-sharded frame (SURVEY §8(f)3;
+ * the reference is single-GPU). d_src is a dense slab of the handle's width x
+ * height (pitch width*3) whose rows [row_lo, row_hi) are valid frame rows: every
+ * stage clamps into them, which at a frame edge is the reference's replicate
+ * border. Writes the iteration's rows [out_row0, out_row0 + out_rows) to d_dst
+ * (row 0 of d_dst = slab row out_row0). Rows further than vip_texture_halo_rows(k)
+ * from the frame edge must be backed by valid neighbour rows in d_src. */
+int vip_texture_halo_rows(int ksize);
+int vip_texture_iterate_rows(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, size_t dst_pitch, int out_row0,
+                             int out_rows, int row_lo, int row_hi, void* stream);
 /* Impl::compute_blur_and_rtv (:216-237): image u8x3, magnitude f32 -> blurred f32x3, rtv f32 */
 int vip_texture_blur_rtv(vip_texture_t h, const uint8_t* d_image, const float* d_magnitude, float* d_blurred,
                          float* d_rtv, void* stream);

@@ -74,10 +74,11 @@ def test_cpp_headers_mirror_reference_signatures():
     assert "void execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst);" in hdr
 
 
-def test_sample_links_against_library():
-    """samples/vip_benchmark (C++ drop-in API consumer) is built and resolves libvip_hip.so."""
+@pytest.mark.parametrize("name", ["vip_benchmark", "vip_host_pipeline"])
+def test_sample_links_against_library(name):
+    """samples/* (C++ drop-in API consumers) are built and resolve libvip_hip.so."""
     import subprocess
-    exe = os.path.join(ROOT, "samples", "vip_benchmark")
+    exe = os.path.join(ROOT, "samples", name)
     if not os.path.exists(exe):
         pytest.skip("sample not built (make -C various_image_processings_amd/csrc samples)")
     out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout

@@ -25,17 +25,18 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, width, height, ksize, adaptive, out_dir):
+def _worker(rank, world, port, width, height, ksize, kind, nitr, out_dir):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from oracle import oracle as o
-    from various_image_processings_amd.sharded import SlabGeometry, exchange_halo
+    from various_image_processings_amd.sharded import SlabGeometry, exchange_halo, texture_halo_rows
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     frame = o.random_image(width, height)
-    geo = SlabGeometry(width, height, ksize // 2, rank, world)
+    halo = nitr * texture_halo_rows(ksize) if kind == "texture" else ksize // 2
+    geo = SlabGeometry(width, height, halo, rank, world)
     b, e = geo.rows
     r = geo.radius
     slab = torch.zeros((geo.slab_rows, width, 3), dtype=torch.uint8)
@@ -50,23 +51,33 @@ def _worker(rank, world, port, width, height, ksize, adaptive, out_dir):
         assert np.array_equal(s[r + geo.own:], frame[e:e + r])
     # the band filter over the clamp range == the frame filter's rows
     view = s[lo:hi]
-    fn = o.adaptive if adaptive else o.bilateral
-    band = fn(np.ascontiguousarray(view), ksize)[r - lo:r - lo + geo.own]
+    if kind == "texture":  # the slab filtered as a frame: its own rows are exact given the halo
+        band = o.texture(np.ascontiguousarray(view), ksize, nitr)[r - lo:r - lo + geo.own]
+    else:
+        fn = o.adaptive if kind == "adaptive" else o.bilateral
+        band = fn(np.ascontiguousarray(view), ksize)[r - lo:r - lo + geo.own]
     np.save(os.path.join(out_dir, f"rank{rank}.npy"), band)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,height,ksize,adaptive", [(2, 37, 9, False), (3, 50, 15, False), (2, 41, 7, True)])
-def test_row_sharded_halo_exchange_matches_full_frame(tmp_path, world, height, ksize, adaptive):
+@pytest.mark.parametrize("world,height,ksize,kind,nitr", [(2, 37, 9, "bilateral", 0), (3, 50, 15, "bilateral", 0),
+                                                          (2, 41, 7, "adaptive", 0), (2, 70, 5, "texture", 3),
+                                                          (3, 90, 3, "texture", 4)])
+def test_row_sharded_halo_exchange_matches_full_frame(tmp_path, world, height, ksize, kind, nitr):
+    """Texture: one exchange of nitr * texture_halo_rows(k) rows per frame
+    (ShardedTexture's ghost-zone scheme) makes each slab's own rows exact."""
     from oracle import oracle as o
     width = 29
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, width, height, ksize, adaptive, str(tmp_path)), nprocs=world,
+    mp.start_processes(_worker, args=(world, port, width, height, ksize, kind, nitr, str(tmp_path)), nprocs=world,
                        join=True, start_method="spawn")
     got = np.concatenate([np.load(tmp_path / f"rank{i}.npy") for i in range(world)], axis=0)
     frame = o.random_image(width, height)
-    want = (o.adaptive if adaptive else o.bilateral)(frame, ksize)
+    if kind == "texture":
+        want = o.texture(frame, ksize, nitr)
+    else:
+        want = (o.adaptive if kind == "adaptive" else o.bilateral)(frame, ksize)
     assert np.array_equal(got, want)
 
 

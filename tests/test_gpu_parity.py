@@ -234,3 +234,82 @@ def test_profiles_within_reference_tolerance(dev, oracle, lenna):
     diff = np.abs(got - want)
     assert diff.max() <= 1
     print(f"exact-match fraction vs include/cpp numerics: {(diff == 0).mean():.6f}")
+
+
+def test_host_frame_async_path(dev, oracle):
+    """Pinned host frame -> vip_upload_async -> bilateral on a vip_stream_create stream
+    -> vip_download_async: the stream-ordered host path gives the
+    same bytes as the oracle."""
+    import ctypes
+    from various_image_processings_amd._lib import call, lib
+    img = oracle.random_image(301, 123)
+    n = img.nbytes
+    h_in, h_out, stream = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    call("vip_host_alloc", ctypes.byref(h_in), n)
+    call("vip_host_alloc", ctypes.byref(h_out), n)
+    call("vip_stream_create", ctypes.byref(stream))
+    try:
+        ctypes.memmove(h_in.value, img.ctypes.data, n)
+        ctypes.memset(h_out.value, 0, n)
+        d_src, d_dst = dev.empty(img.shape), dev.empty(img.shape)
+        f = _BilateralImpl(301, 123, 9)
+        call("vip_upload_async", ctypes.c_void_p(d_src.data_ptr()), h_in, n, stream)
+        f.bilateral_filter(d_src, d_dst, stream=stream.value)
+        call("vip_download_async", h_out, ctypes.c_void_p(d_dst.data_ptr()), n, stream)
+        call("vip_stream_synchronize", stream)
+        got = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(h_out.value)).reshape(img.shape).copy()
+    finally:
+        call("vip_stream_destroy", stream)
+        call("vip_host_free", h_in)
+        call("vip_host_free", h_out)
+    want = oracle.bilateral(img, 9)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+def _fill_slab(dev, frame, geo):
+    """The slab a rank holds after exchange_halo: own rows plus neighbour halo rows."""
+    import torch
+    b, e = geo.rows
+    r = geo.radius
+    slab = np.zeros((geo.slab_rows, frame.shape[1], 3), np.uint8)
+    slab[r:r + geo.own] = frame[b:e]
+    if geo.has_above:
+        slab[:r] = frame[b - r:b]
+    if geo.has_below:
+        slab[r + geo.own:] = frame[e:e + r]
+    return dev.put(slab)
+
+
+@pytest.mark.parametrize("world,shape,k,nitr,numerics", [(3, (100, 70), 5, 3, 0), (2, (64, 130), 3, 5, 1),
+                                                         (4, (201, 67), 5, 2, 0), (1, (40, 33), 5, 5, 0)])
+def test_sharded_texture_matches_full_frame(dev, oracle, world, shape, k, nitr, numerics):
+    """ShardedTexture (one halo exchange of nitr * texture_halo_rows(k) rows, then
+    shrinking ghost zones through vip_texture_iterate_rows) on every rank's slab ==
+    the full-frame texture filter."""
+    from various_image_processings_amd.sharded import ShardedTexture
+    h, w = shape
+    frame = oracle.random_image(w, h)
+    parts = []
+    for rank in range(world):
+        st = ShardedTexture(w, h, k, nitr, rank, world, numerics=numerics)
+        slab = _fill_slab(dev, frame, st.geo)
+        out = dev.empty((st.geo.own, w, 3))
+        st.filter(slab, out, exchange=False)
+        parts.append(dev.get(out))
+    got = np.concatenate(parts, axis=0)
+    want = oracle.texture(frame, k, nitr, profile=numerics)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+def test_texture_iterate_rows_band(dev, oracle):
+    """One vip_texture_iterate_rows call over a middle row band of a whole frame
+    (valid rows = the frame) == those rows of a one-iteration texture filter."""
+    h, w, k = 90, 77, 5
+    frame = oracle.random_image(w, h)
+    f = _TextureImpl(w, h, k, 1)
+    d_src = dev.put(frame)
+    band = dev.empty((31, w, 3))
+    f.iterate_rows(d_src, band, 40, 31, 0, h)
+    want = oracle.texture(frame, k, 1)
+    got = dev.get(band)
+    assert np.array_equal(got, want[40:71]), _mismatch(got, want[40:71])

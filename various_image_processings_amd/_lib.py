@@ -36,6 +36,12 @@ SIGNATURES = {
     "vip_download": (_c_int, [_c_void_p, _c_void_p, _c_size_t]),
     "vip_device_synchronize": (_c_int, []),
     "vip_stream_synchronize": (_c_int, [_c_void_p]),
+    "vip_host_alloc": (_c_int, [ctypes.POINTER(_c_void_p), _c_size_t]),
+    "vip_host_free": (_c_int, [_c_void_p]),
+    "vip_upload_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
+    "vip_download_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
+    "vip_stream_create": (_c_int, [ctypes.POINTER(_c_void_p)]),
+    "vip_stream_destroy": (_c_int, [_c_void_p]),
     "vip_bilateral_create": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_int, _c_float, _c_float, _c_int]),
     "vip_bilateral_destroy": (_c_int, [_c_void_p]),
     "vip_bilateral_run": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p, _c_size_t, _c_void_p]),
@@ -54,6 +60,9 @@ SIGNATURES = {
     "vip_texture_create": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_int, _c_int, _c_int]),
     "vip_texture_destroy": (_c_int, [_c_void_p]),
     "vip_texture_run": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "vip_texture_halo_rows": (_c_int, [_c_int]),
+    "vip_texture_iterate_rows": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_int, _c_int, _c_int,
+                                          _c_void_p]),
     "vip_texture_blur_rtv": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "vip_texture_guide": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
 }

@@ -36,6 +36,8 @@ int launch_guide(const float* blurred, const float* rtv, uint8_t* guide, int wid
                  hipStream_t stream);
 int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, bool cpp,
                                hipStream_t stream);
+int launch_texture_guide_fused_rows(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
+                                    int ksize, bool cpp, hipStream_t stream);
 
 // LUT construction. CUDA profile: src/bilateral_filter_impl.cu:217-237 (float
 // coefficient, std::exp(float) == expf). CPP profile: include/cpp/bilateral_filter.hpp:13-36
@@ -149,6 +151,22 @@ int vip_download(void* h_dst, const void* d_src, size_t bytes) {
 }
 int vip_device_synchronize(void) { return (int)hipDeviceSynchronize(); }
 int vip_stream_synchronize(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
+int vip_host_alloc(void** h_ptr, size_t bytes) {
+    if (!h_ptr) return VIP_ERR_INVALID_ARGUMENT;
+    return (int)hipHostMalloc(h_ptr, bytes, hipHostMallocDefault);
+}
+int vip_host_free(void* h_ptr) { return (int)hipHostFree(h_ptr); }
+int vip_upload_async(void* d_dst, const void* h_src, size_t bytes, void* stream) {
+    return (int)hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+}
+int vip_download_async(void* h_dst, const void* d_src, size_t bytes, void* stream) {
+    return (int)hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+int vip_stream_create(void** stream) {
+    if (!stream) return VIP_ERR_INVALID_ARGUMENT;
+    return (int)hipStreamCreateWithFlags(reinterpret_cast<hipStream_t*>(stream), hipStreamNonBlocking);
+}
+int vip_stream_destroy(void* stream) { return (int)hipStreamDestroy((hipStream_t)stream); }
 
 // ---------------------------------------------------------------- bilateral
 int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
@@ -349,6 +367,39 @@ int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void*
         cur = next;
     }
     return 0;
+}
+
+int vip_texture_halo_rows(int ksize) {
+    if (ksize < 1) return VIP_ERR_INVALID_ARGUMENT;
+    // JBF radius (2k-1)/2 = k-1 on the guide, whose stages reach gradient 1 + blur/mRTV
+    // k/2 + argmin k/2 rows further into the image
+    return (ksize - 1) + 2 * (ksize / 2) + 1;
+}
+
+// One iteration on a row slab (multi-GPU texture filter): guide rows
+// [out_row0 - (k-1), out_row0 + out_rows + (k-1)) clipped to the valid rows, then
+// the JBF of the output rows. Stage reads clamp into [row_lo, row_hi), so at a
+// frame edge the result is the reference's; elsewhere the caller supplies
+// vip_texture_halo_rows(k) valid rows around the output rows.
+int vip_texture_iterate_rows(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, size_t dst_pitch, int out_row0,
+                             int out_rows, int row_lo, int row_hi, void* stream) {
+    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi ||
+        out_row0 < row_lo || out_row0 + out_rows > row_hi)
+        return VIP_ERR_INVALID_ARGUMENT;
+    if (out_rows == 0) return 0;
+    const size_t pitch = (size_t)h->width * 3;
+    const uint8_t* dst_end = d_dst + (size_t)(out_rows - 1) * dst_pitch + pitch;
+    const uint8_t* src_end = d_src + (size_t)h->height * pitch;
+    if (d_dst < src_end && dst_end > d_src) return VIP_ERR_ALIASING;
+    const int rj = h->ksize - 1;
+    const int g0 = out_row0 - rj > row_lo ? out_row0 - rj : row_lo;
+    const int g1 = out_row0 + out_rows + rj < row_hi ? out_row0 + out_rows + rj : row_hi;
+    const hipStream_t s = (hipStream_t)stream;
+    int rc = launch_texture_guide_fused_rows(d_src, h->d_guide, h->width, row_lo, row_hi, g0, g1, h->ksize,
+                                             h->numerics == VIP_NUMERICS_CPP, s);
+    if (!rc) rc = vip_bilateral_run_rows(h->jbf, d_src, pitch, h->d_guide, pitch, d_dst, dst_pitch, out_rows,
+                                         out_row0, row_lo, row_hi, stream);
+    return rc;
 }
 
 }  // extern "C"

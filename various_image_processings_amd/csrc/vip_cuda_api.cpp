@@ -40,14 +40,23 @@ CudaBilateralFilter::Impl::Impl(const int width, const int height, const int ksi
 CudaBilateralFilter::Impl::~Impl() { vip_bilateral_destroy(handle_); }
 
 void CudaBilateralFilter::Impl::bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst) const {
-    VIP_REPORT(vip_bilateral_run(handle_, d_src, (size_t)width_ * 3, d_dst, (size_t)width_ * 3, nullptr));
+    bilateral_filter(d_src, d_dst, nullptr);
+}
+void CudaBilateralFilter::Impl::bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst,
+                                                 void* stream) const {
+    VIP_REPORT(vip_bilateral_run(handle_, d_src, (size_t)width_ * 3, d_dst, (size_t)width_ * 3, stream));
 }
 
 void CudaBilateralFilter::Impl::joint_bilateral_filter(const std::uint8_t* const d_src,
                                                        const std::uint8_t* const d_guide,
                                                        std::uint8_t* const d_dst) const {
+    joint_bilateral_filter(d_src, d_guide, d_dst, nullptr);
+}
+void CudaBilateralFilter::Impl::joint_bilateral_filter(const std::uint8_t* const d_src,
+                                                       const std::uint8_t* const d_guide, std::uint8_t* const d_dst,
+                                                       void* stream) const {
     const size_t pitch = (size_t)width_ * 3;
-    VIP_REPORT(vip_joint_bilateral_run(handle_, d_src, pitch, d_guide, pitch, d_dst, pitch, nullptr));
+    VIP_REPORT(vip_joint_bilateral_run(handle_, d_src, pitch, d_guide, pitch, d_dst, pitch, stream));
 }
 
 CudaBilateralFilter::CudaBilateralFilter(const int width, const int height, const int ksize, const float sigma_space,
@@ -66,6 +75,16 @@ void CudaBilateralFilter::joint_bilateral_filter(const std::uint8_t* const d_src
     VIP_REPORT(vip_device_synchronize());
 }
 
+void CudaBilateralFilter::bilateral_filter(const std::uint8_t* const d_src, std::uint8_t* const d_dst,
+                                           void* stream) const {
+    impl_->bilateral_filter(d_src, d_dst, stream);
+}
+
+void CudaBilateralFilter::joint_bilateral_filter(const std::uint8_t* const d_src, const std::uint8_t* const d_guide,
+                                                 std::uint8_t* const d_dst, void* stream) const {
+    impl_->joint_bilateral_filter(d_src, d_guide, d_dst, stream);
+}
+
 // ------------------------------------------------------------ CudaAdaptiveBilateralFilter
 CudaAdaptiveBilateralFilter::Impl::Impl(const int width, const int height, const int ksize, const float sigma_space,
                                         const float sigma_color)
@@ -77,7 +96,11 @@ CudaAdaptiveBilateralFilter::Impl::Impl(const int width, const int height, const
 CudaAdaptiveBilateralFilter::Impl::~Impl() { vip_adaptive_destroy(handle_); }
 
 void CudaAdaptiveBilateralFilter::Impl::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst) const {
-    VIP_REPORT(vip_adaptive_run(handle_, d_src, (size_t)width_ * 3, d_dst, (size_t)width_ * 3, nullptr));
+    execute(d_src, d_dst, nullptr);
+}
+void CudaAdaptiveBilateralFilter::Impl::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst,
+                                                void* stream) const {
+    VIP_REPORT(vip_adaptive_run(handle_, d_src, (size_t)width_ * 3, d_dst, (size_t)width_ * 3, stream));
 }
 
 CudaAdaptiveBilateralFilter::CudaAdaptiveBilateralFilter(const int width, const int height, const int ksize,
@@ -90,6 +113,11 @@ void CudaAdaptiveBilateralFilter::execute(const std::uint8_t* const d_src, std::
     VIP_REPORT(vip_device_synchronize());
 }
 
+void CudaAdaptiveBilateralFilter::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst,
+                                          void* stream) const {
+    impl_->execute(d_src, d_dst, stream);
+}
+
 // ------------------------------------------------------------ CudaBilateralTextureFilter
 CudaBilateralTextureFilter::Impl::Impl(const int width, const int height, const int ksize, const int nitr) {
     const int rc = vip_texture_create(&handle_, width, height, ksize, nitr, VIP_NUMERICS_CUDA);
@@ -98,7 +126,11 @@ CudaBilateralTextureFilter::Impl::Impl(const int width, const int height, const 
 CudaBilateralTextureFilter::Impl::~Impl() { vip_texture_destroy(handle_); }
 
 void CudaBilateralTextureFilter::Impl::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst) {
-    VIP_REPORT(vip_texture_run(handle_, d_src, d_dst, nullptr));
+    execute(d_src, d_dst, nullptr);
+}
+void CudaBilateralTextureFilter::Impl::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst,
+                                               void* stream) {
+    VIP_REPORT(vip_texture_run(handle_, d_src, d_dst, stream));
 }
 
 void CudaBilateralTextureFilter::Impl::compute_blur_and_rtv(const std::uint8_t* d_image, const float* d_magnitude,
@@ -119,6 +151,10 @@ CudaBilateralTextureFilter::~CudaBilateralTextureFilter() = default;
 void CudaBilateralTextureFilter::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst) {
     impl_->execute(d_src, d_dst);
     VIP_REPORT(vip_device_synchronize());
+}
+
+void CudaBilateralTextureFilter::execute(const std::uint8_t* const d_src, std::uint8_t* const d_dst, void* stream) {
+    impl_->execute(d_src, d_dst, stream);
 }
 
 // ------------------------------------------------------------ cuda_gradient
@@ -145,6 +181,12 @@ public:
     ~Impl() { vip_free(data_); }
     void upload(const ElemType* const data) { VIP_REPORT(vip_upload(data_, data, len_ * sizeof(ElemType))); }
     void download(ElemType* const data) { VIP_REPORT(vip_download(data, data_, len_ * sizeof(ElemType))); }
+    void upload_async(const ElemType* const data, void* stream) {
+        VIP_REPORT(vip_upload_async(data_, data, len_ * sizeof(ElemType), stream));
+    }
+    void download_async(ElemType* const data, void* stream) {
+        VIP_REPORT(vip_download_async(data, data_, len_ * sizeof(ElemType), stream));
+    }
     ElemType* get() { return data_; }
 
 private:
@@ -162,6 +204,21 @@ DeviceImage<ElemType>::~DeviceImage() {
 }
 
 template <typename ElemType>
+DeviceImage<ElemType>::DeviceImage(DeviceImage&& other) noexcept : impl_(other.impl_) {
+    other.impl_ = nullptr;
+}
+
+template <typename ElemType>
+DeviceImage<ElemType>& DeviceImage<ElemType>::operator=(DeviceImage&& other) noexcept {
+    if (this != &other) {
+        delete impl_;
+        impl_ = other.impl_;
+        other.impl_ = nullptr;
+    }
+    return *this;
+}
+
+template <typename ElemType>
 void DeviceImage<ElemType>::upload(const ElemType* const data) {
     impl_->upload(data);
 }
@@ -174,6 +231,16 @@ void DeviceImage<ElemType>::download(ElemType* const data) {
 template <typename ElemType>
 ElemType* DeviceImage<ElemType>::get() {
     return impl_->get();
+}
+
+template <typename ElemType>
+void DeviceImage<ElemType>::upload_async(const ElemType* const data, void* stream) {
+    impl_->upload_async(data, stream);
+}
+
+template <typename ElemType>
+void DeviceImage<ElemType>::download_async(ElemType* const data, void* stream) {
+    impl_->download_async(data, stream);
 }
 
 template class DeviceImage<std::uint8_t>;

@@ -262,10 +262,15 @@ struct GfGeom {
     static constexpr int WORDS = XW * XH + MW * MH + 4 * BW * BH;
 };
 
+// Row bands: rows [lo, hi) of the (dense, width*3 pitch) buffers are the valid
+// frame rows -- every stage clamps into them, as the reference clamps into
+// [0, height) -- and guide rows [gy0, gy1) are produced (a row slab of a sharded
+// frame; the whole frame is lo = gy0 = 0, hi = gy1 = height).
 template <int R, bool CPP>
 __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
-                                                                   uint8_t* __restrict__ guide, int width,
-                                                                   int height, int ksize, int aligned) {
+                                                                   uint8_t* __restrict__ guide, int width, int lo,
+                                                                   int hi, int gy0, int gy1, int ksize,
+                                                                   int aligned) {
     using G = GfGeom<R>;
     constexpr int K = 2 * R + 1;  // window width; the reference divides by ksize^2 and
                                   // uses sigma_alpha = 1/(5 ksize) even when ksize is even
@@ -275,18 +280,18 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     float* MR = reinterpret_cast<float*>(XR + G::XW * G::XH);
     float* BR = MR + G::MW * G::MH;  // 3 planes of BW*BH
     float* RR = BR + 3 * G::BW * G::BH;
-    const int x0 = blockIdx.x * kGfTW, y0 = blockIdx.y * kGfTH;
+    const int x0 = blockIdx.x * kGfTW, y0 = gy0 + blockIdx.y * kGfTH;
     const int tid = threadIdx.x;
     // region origins (image coordinates)
     const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
     const int mr0x = x0 - 2 * R, mr0y = y0 - 2 * R;
     const int br0x = x0 - R, br0y = y0 - R;
-    const int W1 = width - 1, H1 = height - 1;
+    const int W1 = width - 1, H0 = lo, H1 = hi - 1;
 
     // 1. XR: 4-pixel groups, dword loads when interior and aligned, clamped bytes otherwise
     for (int g = tid; g < G::XH * (G::XW / 4); g += kGfNT) {
         const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
-        const uint8_t* row = img + (long long)clampi(yr0 + ry, 0, H1) * width * 3;
+        const uint8_t* row = img + (long long)clampi(yr0 + ry, H0, H1) * width * 3;
         const int x = xr0 + 4 * gx;
         uint4 q;
         if (aligned && x >= 0 && x + 3 <= W1) {
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //    are read directly (XR[c +- e] == X(clamp(c +- e)))
     for (int i = tid; i < G::MW * G::MH; i += kGfNT) {
         const int qy = i / G::MW, qx = i - qy * G::MW;
-        const int cx = clampi(mr0x + qx, 0, W1) - xr0, cy = clampi(mr0y + qy, 0, H1) - yr0;
+        const int cx = clampi(mr0x + qx, 0, W1) - xr0, cy = clampi(mr0y + qy, H0, H1) - yr0;
         const uint32_t* c = XR + cy * G::XW + cx;
         const uint32_t L = c[-1], Rt = c[1], U = c[-G::XW], D = c[G::XW];
         float dx = 0.f, dy = 0.f;
@@ -334,7 +339,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
             smin[j] = 0xffffffffu;
             mmax[j] = msum[j] = 0.f;
         }
-        if (iy >= 0 && iy <= H1 && ix0 >= 0 && ix0 + kGfRun - 1 <= W1) {
+        if (iy >= H0 && iy <= H1 && ix0 >= 0 && ix0 + kGfRun - 1 <= W1) {
             // all centres inside the image: shared row segments
             for (int ky = -R; ky <= R; ++ky) {
                 const uint32_t* xrow = XR + (iy + ky - yr0) * G::XW + (ix0 - R - xr0);
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
         } else {
 #pragma unroll
             for (int j = 0; j < kGfRun; ++j) {
-                const int cx = clampi(ix0 + j, 0, W1), cy = clampi(iy, 0, H1);
+                const int cx = clampi(ix0 + j, 0, W1), cy = clampi(iy, H0, H1);
                 for (int ky = -R; ky <= R; ++ky) {
                     const uint32_t* xrow = XR + (cy + ky - yr0) * G::XW + (cx - xr0);
                     const float* mrow = MR + (cy + ky - mr0y) * G::MW + (cx - mr0x);
@@ -416,7 +421,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     for (int run = tid; run < (kGfTH / kGfRun) * kGfTW; run += kGfNT) {
         const int tx = run % kGfTW, ty0 = (run / kGfTW) * kGfRun;
         const int x = x0 + tx;
-        if (x > W1 || y0 + ty0 > H1) continue;
+        if (x > W1 || y0 + ty0 >= gy1) continue;
         float rv[kGfRun + 2 * R];
         int ri[kGfRun + 2 * R];
 #pragma unroll
@@ -437,7 +442,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 #pragma unroll
         for (int j = 0; j < kGfRun; ++j) {
             const int y = y0 + ty0 + j;
-            if (y > H1) break;
+            if (y >= gy1) break;
             float rmin = CPP ? 3.402823466e+38f : 1e10f;
             int mi = 0;
 #pragma unroll
@@ -464,8 +469,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 }
 
 template <int R, bool CPP>
-static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, int aligned,
-                     hipStream_t stream) {
+static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1, int ksize,
+                     int aligned, hipStream_t stream) {
     constexpr int LDS = 4 * GfGeom<R>::WORDS;
     static_assert(LDS <= kLdsBudget, "fused guide tile does not fit LDS");
     auto kern = texture_guide_fused_kernel<R, CPP>;
@@ -475,32 +480,38 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int height, 
                                           hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
         attr_done = true;
     }
-    dim3 grid((width + kGfTW - 1) / kGfTW, (height + kGfTH - 1) / kGfTH);
-    hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, height, ksize, aligned);
+    if (gy1 <= gy0) return 0;
+    dim3 grid((width + kGfTW - 1) / kGfTW, (gy1 - gy0 + kGfTH - 1) / kGfTH);
+    hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
     return (int)hipGetLastError();
 }
 
 template <bool CPP>
-static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width, int height, int aligned,
-                       hipStream_t s) {
+static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
+                       int aligned, hipStream_t s) {
     switch (ksize / 2) {
-        case 1: return launch_gf<1, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 2: return launch_gf<2, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 3: return launch_gf<3, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 4: return launch_gf<4, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 5: return launch_gf<5, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 6: return launch_gf<6, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 7: return launch_gf<7, CPP>(img, guide, width, height, ksize, aligned, s);
-        case 8: return launch_gf<8, CPP>(img, guide, width, height, ksize, aligned, s);
+        case 1: return launch_gf<1, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 2: return launch_gf<2, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 3: return launch_gf<3, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 4: return launch_gf<4, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 5: return launch_gf<5, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 6: return launch_gf<6, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 7: return launch_gf<7, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 8: return launch_gf<8, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         default: return VIP_ERR_UNSUPPORTED_KSIZE;
     }
 }
 
+int launch_texture_guide_fused_rows(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
+                                    int ksize, bool cpp, hipStream_t stream) {
+    const int aligned = ((uintptr_t)img % 4 == 0) && ((size_t)width * 3 % 4 == 0);
+    return cpp ? launch_gf_r<true>(ksize, img, guide, width, lo, hi, gy0, gy1, aligned, stream)
+               : launch_gf_r<false>(ksize, img, guide, width, lo, hi, gy0, gy1, aligned, stream);
+}
+
 int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, bool cpp,
                                hipStream_t stream) {
-    const int aligned = ((uintptr_t)img % 4 == 0) && ((size_t)width * 3 % 4 == 0);
-    return cpp ? launch_gf_r<true>(ksize, img, guide, width, height, aligned, stream)
-               : launch_gf_r<false>(ksize, img, guide, width, height, aligned, stream);
+    return launch_texture_guide_fused_rows(img, guide, width, 0, height, 0, height, ksize, cpp, stream);
 }
 
 }  // namespace vip

@@ -169,6 +169,12 @@ class _TextureImpl(_Handle):
     def compute_guide(self, d_blurred, d_rtv, d_guide, stream=None):
         call("vip_texture_guide", self._h, _ptr(d_blurred), _ptr(d_rtv), _ptr(d_guide), _stream(stream))
 
+    def iterate_rows(self, d_src, d_dst, out_row0, out_rows, row_lo, row_hi, stream=None):
+        """One iteration on a row slab (include/vip.h vip_texture_iterate_rows): d_dst
+        receives slab rows [out_row0, out_row0 + out_rows)."""
+        call("vip_texture_iterate_rows", self._h, _ptr(d_src), _ptr(d_dst), self.width * 3, int(out_row0),
+             int(out_rows), int(row_lo), int(row_hi), _stream(stream))
+
 
 class CudaBilateralTextureFilter:
     """include/cuda/bilateral_texture_filter.hpp:7-17."""
