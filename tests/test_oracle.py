@@ -176,3 +176,26 @@ def test_numpy_restatement_blur_rtv_guide(oracle):
                 v = np.float32(np.float64(alpha) * np.float64(b[by, bx, c]) + np.float64(prod))  # exact fma
                 v = np.float32(v + np.float32(0.5))
                 assert g[y, x, c] == min(max(int(v), 0), 255), (y, x, c)
+
+
+def _fma32(a, b, c):
+    """float32 fma, exact through long double: every product/sum below spans < 64 bits."""
+    ld = np.longdouble
+    return (ld(a) * ld(b) + ld(c)).astype(np.float32)
+
+
+@pytest.mark.skipif(np.finfo(np.longdouble).nmant < 63, reason="needs x87 80-bit long double")
+def test_constant_division_is_exact():
+    """The fused texture guide stage (vip_texture.hip div_exact) divides the integer
+    box sums by ksize^2 and the intensity byte sums by 3 with an fma-corrected
+    reciprocal: q0 = s*rd, q = fma(fma(-q0, d, s), rd, q0). It must equal the correctly
+    rounded float quotient the reference computes (src/bilateral_texture_filter_impl.cu:
+    97-100, :84) for EVERY reachable numerator -- checked exhaustively here."""
+    cases = [((2 * (k // 2) + 1) ** 2 * 255, k * k) for k in range(2, 18)] + [(765, 3)]
+    for smax, d in cases:
+        s = np.arange(smax + 1, dtype=np.float32)
+        d32 = np.float32(d)
+        rd = np.float32(1) / d32
+        q0 = (s * rd).astype(np.float32)
+        q = _fma32(_fma32(-q0, d32, s), rd, q0)
+        assert np.array_equal(q, (s / d32).astype(np.float32)), d

@@ -239,28 +239,100 @@ namespace vip {
 // the reference stage reads through its own clamped coordinates. Inner loops then
 // index the regions directly; a position outside the image only clamps its
 // centre once.
-//   XR : T (+) (2R+1)  image pixels as RGBX words (origin 4-px aligned)
-//   MR : T (+) 2R      gradient magnitude
-//   BR, RR : T (+) R   blurred RGB and rtv
-// Bit-exact with the stage kernels: integer box sums (exact), intensity extremes
-// from integer byte sums (x/3.f is monotonic), magnitude sum accumulated in the
-// reference's row-major order, rtv divide in double (CUDA profile).
+//   XR : image pixels as RGBX words, T (+) (2R+1) (origin 4-px aligned)
+//   MR : gradient magnitude, T (+) 2R
+//   H  : horizontal window aggregates of the image rows of T (+) 2R at the blur
+//        columns of T (+) R: {R|B<<16 sums, G sums, max|(1023-min)<<16 of the
+//        byte sums r+g+b} -- the separable part of the box blur and of the
+//        intensity extremes (integer sums and max/min are order-free, so exact)
+//   BR, RR : blurred RGB and rtv, T (+) R (aliases XR/H once those are consumed)
+// The magnitude sum is NOT separable: it is accumulated per blur position in the
+// reference's row-major order. Bit-exact with the stage kernels: x/3.f is
+// monotonic (extremes of integer sums), float divides by the constants ksize^2
+// and 3 use an fma-corrected reciprocal that equals the correctly rounded
+// quotient on every reachable numerator (verified exhaustively,
+// tests/test_oracle.py::test_constant_division_is_exact), rtv divide in double
+// (CUDA profile).
 // ---------------------------------------------------------------------------
-constexpr int kGfTW = 64, kGfTH = 16, kGfNT = 256, kGfRun = 4;
+constexpr int kGfTW = 64, kGfTH = 16, kGfNT = 256;
+constexpr int kGfH1 = 8;   // pass 1: horizontally adjacent window aggregates per thread
+constexpr int kGfV2 = 4;   // pass 2: vertically adjacent blur positions per thread
+constexpr int kGfRun = 4;  // guide: vertically adjacent outputs per thread
+
+constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <int R>
 struct GfGeom {
-    static constexpr int XL = round_up(2 * R + 1, 4);          // XR left apron (aligned)
-    // widths padded so the runs of kGfRun positions that overhang the real
-    // regions (their results are never read) stay inside their source rows
-    static constexpr int XW = round_up(kGfTW + XL + 2 * R + 1 + 8, 4);
-    static constexpr int XH = kGfTH + 4 * R + 2;
-    static constexpr int MW = round_up(kGfTW + 4 * R + 4, kGfRun);
-    static constexpr int MH = kGfTH + 4 * R;
-    static constexpr int BW = round_up(kGfTW + 2 * R, kGfRun);
+    static constexpr int K = 2 * R + 1;
+    static constexpr int BW = kGfTW + 2 * R;            // BR/RR: T (+) R
     static constexpr int BH = kGfTH + 2 * R;
-    static constexpr int WORDS = XW * XH + MW * MH + 4 * BW * BH;
+    static constexpr int BHP = round_up(BH, kGfV2);     // + pass-2 overhang rows
+    static constexpr int HWP = round_up(BW, kGfH1);     // H: blur columns, rows of T (+) 2R
+    static constexpr int HH = BHP + 2 * R;
+    static constexpr int MW = round_up(BW + 2 * R, 4);  // MR: T (+) 2R
+    static constexpr int MH = HH;
+    static constexpr int XL = round_up(2 * R + 1, 4);   // XR left apron (4-px aligned origin)
+    static constexpr int XW = round_up(cmax(MW - 2 * R + XL + 1, HWP + XL), 4);
+    static constexpr int XH = MH + 2;
+    static constexpr int XR_WORDS = XW * XH;
+    static constexpr int HPL = HWP * HH;                // one H plane
+    static constexpr int BPL = BW * BHP;                // one BR/RR plane
+    static constexpr int A_WORDS = cmax(XR_WORDS + 3 * HPL, 4 * BPL);
+    static constexpr int WORDS = A_WORDS + MW * MH;
+    static constexpr int NR1 = HH * (HWP / kGfH1);      // pass-1 runs
+    static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
+    static constexpr int IT2 = (NR2 + kGfNT - 1) / kGfNT;
 };
+
+typedef short gf_s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short gf_u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(gf_u16x2, a),
+                                                                  __builtin_bit_cast(gf_u16x2, b)));
+}
+
+// N sliding sums of K consecutive terms of x (integer: the add/subtract slide is exact)
+template <int N, int K>
+__device__ __forceinline__ void win_sum(const uint32_t (&x)[N + K - 1], uint32_t (&o)[N]) {
+    uint32_t s = x[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) s += x[k];
+    o[0] = s;
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        s = s + x[j + K - 1] - x[j - 1];
+        o[j] = s;
+    }
+}
+
+// N sliding maxima (any associative, idempotent op) of K consecutive terms: blocks of
+// K, suffix scans inside a block and prefix scans into the next, window j =
+// op(suffix[j], prefix[j + K - 1]) (van Herk / Gil-Werman).
+template <int N, int K, class T, class Op>
+__device__ __forceinline__ void win_op(const T (&x)[N + K - 1], T (&o)[N], Op op) {
+    constexpr int M = N + K - 1;
+    T suf[M], pre[M];
+#pragma unroll
+    for (int b0 = 0; b0 < M; b0 += K) {
+        const int b1 = (b0 + K < M ? b0 + K : M) - 1;
+        suf[b1] = x[b1];
+#pragma unroll
+        for (int t = b1 - 1; t >= b0; --t) suf[t] = op(x[t], suf[t + 1]);
+        pre[b0] = x[b0];
+#pragma unroll
+        for (int t = b0 + 1; t <= b1; ++t) pre[t] = op(pre[t - 1], x[t]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; ++j) o[j] = (j % K == 0) ? suf[j] : op(suf[j], pre[j + K - 1]);
+}
+
+// correctly rounded (float)s / d for the reachable integer numerators s (see header)
+__device__ __forceinline__ float div_exact(uint32_t s, float d, float rd) {
+    const float f = (float)s;
+    const float q0 = f * rd;
+    return __builtin_fmaf(__builtin_fmaf(-q0, d, f), rd, q0);
+}
 
 // Row bands: rows [lo, hi) of the (dense, width*3 pitch) buffers are the valid
 // frame rows -- every stage clamps into them, as the reference clamps into
@@ -272,20 +344,20 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
                                                                    int hi, int gy0, int gy1, int ksize,
                                                                    int aligned) {
     using G = GfGeom<R>;
-    constexpr int K = 2 * R + 1;  // window width; the reference divides by ksize^2 and
-                                  // uses sigma_alpha = 1/(5 ksize) even when ksize is even
-    constexpr bool PACKRB = K * K * 255 < 65536;
+    constexpr int K = G::K;  // window width; the reference divides by ksize^2 and
+                             // uses sigma_alpha = 1/(5 ksize) even when ksize is even
+    constexpr bool PACKRB = K * K * 255 < 65536;  // R|B<<16 vertical sums stay in 16 bits
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* XR = lds;
-    float* MR = reinterpret_cast<float*>(XR + G::XW * G::XH);
-    float* BR = MR + G::MW * G::MH;  // 3 planes of BW*BH
-    float* RR = BR + 3 * G::BW * G::BH;
+    uint32_t* H = lds + G::XR_WORDS;                    // 3 planes of HPL
+    float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
+    float* RR = BR + 3 * G::BPL;
+    float* MR = reinterpret_cast<float*>(lds + G::A_WORDS);
     const int x0 = blockIdx.x * kGfTW, y0 = gy0 + blockIdx.y * kGfTH;
     const int tid = threadIdx.x;
     // region origins (image coordinates)
     const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
     const int mr0x = x0 - 2 * R, mr0y = y0 - 2 * R;
-    const int br0x = x0 - R, br0y = y0 - R;
     const int W1 = width - 1, H0 = lo, H1 = hi - 1;
 
     // 1. XR: 4-pixel groups, dword loads when interior and aligned, clamped bytes otherwise
@@ -307,107 +379,176 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     }
     __syncthreads();
 
-    // 2. MR[q] = gradient at c = clamp(q); XR is pre-clamped, so c's neighbours
-    //    are read directly (XR[c +- e] == X(clamp(c +- e)))
+    // 2a. MR[q] = gradient at c = clamp(q); XR is pre-clamped, so c's neighbours are
+    //     read directly (XR[c +- e] == X(clamp(c +- e))). sum_c h^2 + v^2 is an exact
+    //     integer (< 2^24), equal to the reference's float sums: v_dot2 on the
+    //     {c0, c2} 16-bit difference pairs, a mad for c1.
     for (int i = tid; i < G::MW * G::MH; i += kGfNT) {
         const int qy = i / G::MW, qx = i - qy * G::MW;
         const int cx = clampi(mr0x + qx, 0, W1) - xr0, cy = clampi(mr0y + qy, H0, H1) - yr0;
         const uint32_t* c = XR + cy * G::XW + cx;
         const uint32_t L = c[-1], Rt = c[1], U = c[-G::XW], D = c[G::XW];
-        float dx = 0.f, dy = 0.f;
+        const gf_s16x2 h02 = __builtin_bit_cast(gf_s16x2, Rt & 0x00ff00ffu) - __builtin_bit_cast(gf_s16x2, L & 0x00ff00ffu);
+        const gf_s16x2 v02 = __builtin_bit_cast(gf_s16x2, D & 0x00ff00ffu) - __builtin_bit_cast(gf_s16x2, U & 0x00ff00ffu);
+        const int h1 = (int)__builtin_amdgcn_ubfe(Rt, 8, 8) - (int)__builtin_amdgcn_ubfe(L, 8, 8);
+        const int v1 = (int)__builtin_amdgcn_ubfe(D, 8, 8) - (int)__builtin_amdgcn_ubfe(U, 8, 8);
+        const int ss = __builtin_amdgcn_sdot2(h02, h02, __builtin_amdgcn_sdot2(v02, v02, h1 * h1 + v1 * v1, false),
+                                              false);
+        MR[i] = __builtin_sqrtf((float)ss);
+    }
+    // 2b. pass 1: H = horizontal K-window aggregates, kGfH1 adjacent columns per thread.
+    //     H row h <-> image row y0 - 2R + h (XR row h + 1); H column c <-> image column
+    //     x0 - R + c, window XR columns c + XL - 2R .. c + XL.
+    for (int run = tid; run < G::NR1; run += kGfNT) {
+        const int hr = run / (G::HWP / kGfH1), hc0 = (run - hr * (G::HWP / kGfH1)) * kGfH1;
+        const uint32_t* xrow = XR + (hr + 1) * G::XW + hc0 + G::XL - 2 * R;
+        constexpr int NX = kGfH1 + K - 1;
+        uint32_t rb[NX], gg[NX], mx[NX];
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) {
-            const int h = (int)((Rt >> (8 * ch)) & 0xffu) - (int)((L >> (8 * ch)) & 0xffu);
-            const int v = (int)((D >> (8 * ch)) & 0xffu) - (int)((U >> (8 * ch)) & 0xffu);
-            dx = dx + (float)(h * h);
-            dy = dy + (float)(v * v);
+        for (int t = 0; t < NX; ++t) {
+            const uint32_t p = xrow[t];
+            const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);  // r + g + b
+            rb[t] = p & 0x00ff00ffu;
+            gg[t] = __builtin_amdgcn_ubfe(p, 8, 8);
+            mx[t] = ((sb ^ 1023u) << 16) | sb;  // max of lo = max s, max of hi = 1023 - min s
         }
-        MR[i] = __builtin_sqrtf(dx + dy);
+        uint32_t orb[kGfH1], og[kGfH1], omx[kGfH1];
+        win_sum<kGfH1, K>(rb, orb);
+        win_sum<kGfH1, K>(gg, og);
+        win_op<kGfH1, K>(mx, omx, pk_max_u16);
+        uint32_t* h = H + hr * G::HWP + hc0;
+#pragma unroll
+        for (int j = 0; j < kGfH1; j += 4) {
+            *reinterpret_cast<uint4*>(h + j) = make_uint4(orb[j], orb[j + 1], orb[j + 2], orb[j + 3]);
+            *reinterpret_cast<uint4*>(h + G::HPL + j) = make_uint4(og[j], og[j + 1], og[j + 2], og[j + 3]);
+            *reinterpret_cast<uint4*>(h + 2 * G::HPL + j) = make_uint4(omx[j], omx[j + 1], omx[j + 2], omx[j + 3]);
+        }
     }
     __syncthreads();
 
-    // 3. box blur + mRTV, kGfRun horizontally adjacent positions per thread
+    // 3. pass 2: blur + mRTV at the BR positions, kGfV2 vertically adjacent positions per
+    //    thread (vertical windows of H, magnitude sums in row-major order). Blur
+    //    position (p, c) <-> image (y0 - R + p, x0 - R + c): H rows p .. p + 2R, column c;
+    //    MR rows p .. p + 2R, columns c .. c + 2R. Results stay in registers until every
+    //    thread is done with H (BR/RR alias it).
     const float kk = (float)(ksize * ksize);
-    for (int run = tid; run < G::BH * (G::BW / kGfRun); run += kGfNT) {
-        const int py = run / (G::BW / kGfRun), px0 = (run - py * (G::BW / kGfRun)) * kGfRun;
-        const int iy = br0y + py, ix0 = br0x + px0;
-        uint32_t s0[kGfRun], s1[kGfRun], smax[kGfRun], smin[kGfRun], s2[kGfRun];
-        float mmax[kGfRun], msum[kGfRun];
+    const float rkk = 1.f / kk;
+    constexpr float kThird = 0x1.555556p-2f;  // RN(1/3)
+    float res[G::IT2][kGfV2][4];
 #pragma unroll
-        for (int j = 0; j < kGfRun; ++j) {
-            s0[j] = s1[j] = s2[j] = smax[j] = 0u;
-            smin[j] = 0xffffffffu;
-            mmax[j] = msum[j] = 0.f;
-        }
-        if (iy >= H0 && iy <= H1 && ix0 >= 0 && ix0 + kGfRun - 1 <= W1) {
-            // all centres inside the image: shared row segments
-            for (int ky = -R; ky <= R; ++ky) {
-                const uint32_t* xrow = XR + (iy + ky - yr0) * G::XW + (ix0 - R - xr0);
-                const float* mrow = MR + (iy + ky - mr0y) * G::MW + (ix0 - R - mr0x);
-                uint32_t xs[kGfRun + 2 * R];
-                float ms[kGfRun + 2 * R];
+    for (int it = 0; it < G::IT2; ++it) {
+        const int run = tid + it * kGfNT;
+        if (G::NR2 % kGfNT != 0 && run >= G::NR2) continue;
+        const int c = run % G::BW, p0 = (run / G::BW) * kGfV2;
+        const int ix = x0 - R + c, iy0 = y0 - R + p0;
+        uint32_t s0[kGfV2], s1[kGfV2], s2[kGfV2], smx[kGfV2];
+        float mmax[kGfV2], msum[kGfV2];
+        if (ix >= 0 && ix <= W1 && iy0 >= H0 && iy0 + kGfV2 - 1 <= H1) {
+            constexpr int NV = kGfV2 + K - 1;
+            uint32_t hrb[NV], hg[NV], hmx[NV];
+            float rowmax[NV];
 #pragma unroll
-                for (int t = 0; t < kGfRun + 2 * R; ++t) {
-                    xs[t] = xrow[t];
-                    ms[t] = mrow[t];
+            for (int t = 0; t < NV; ++t) {
+                hrb[t] = H[(p0 + t) * G::HWP + c];
+                hg[t] = H[G::HPL + (p0 + t) * G::HWP + c];
+                hmx[t] = H[2 * G::HPL + (p0 + t) * G::HWP + c];
+            }
+            if constexpr (PACKRB) {
+                win_sum<kGfV2, K>(hrb, s0);
+            } else {
+                uint32_t hr_[NV], hb_[NV];
+#pragma unroll
+                for (int t = 0; t < NV; ++t) {
+                    hr_[t] = hrb[t] & 0xffffu;
+                    hb_[t] = hrb[t] >> 16;
                 }
+                win_sum<kGfV2, K>(hr_, s0);
+                win_sum<kGfV2, K>(hb_, s2);
+            }
+            win_sum<kGfV2, K>(hg, s1);
+            win_op<kGfV2, K>(hmx, smx, pk_max_u16);
 #pragma unroll
-                for (int kx = 0; kx < K; ++kx) {
+            for (int j = 0; j < kGfV2; ++j) msum[j] = 0.f;
 #pragma unroll
-                    for (int j = 0; j < kGfRun; ++j) {
-                        const uint32_t p = xs[j + kx];
-                        if constexpr (PACKRB) {
-                            s0[j] += p & 0x00ff00ffu;  // R | B<<16 in 16-bit lanes
-                        } else {
-                            s0[j] += p & 0xffu;
-                            s2[j] += __builtin_amdgcn_ubfe(p, 16, 8);
-                        }
-                        s1[j] += __builtin_amdgcn_ubfe(p, 8, 8);
-                        const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);
-                        smax[j] = sb > smax[j] ? sb : smax[j];
-                        smin[j] = sb < smin[j] ? sb : smin[j];
-                        const float m = ms[j + kx];
-                        mmax[j] = __builtin_fmaxf(mmax[j], m);  // == the reference's max for non-NaN
-                        msum[j] = msum[j] + m;  // row-major order, as the reference
-                    }
+            for (int t = 0; t < NV; ++t) {
+                const float* mrow = MR + (p0 + t) * G::MW + c;
+                float m[K];
+#pragma unroll
+                for (int kx = 0; kx < K; ++kx) m[kx] = mrow[kx];
+                float mx = m[0];
+#pragma unroll
+                for (int kx = 1; kx < K; ++kx) mx = __builtin_fmaxf(mx, m[kx]);  // == the reference's max (no NaN)
+                rowmax[t] = mx;
+                // window row t - j of output j, in the reference's row-major order
+#pragma unroll
+                for (int j = 0; j < kGfV2; ++j) {
+                    if (t - j < 0 || t - j >= K) continue;
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) msum[j] = msum[j] + m[kx];
                 }
             }
+            win_op<kGfV2, K>(rowmax, mmax, [](float a, float b) { return __builtin_fmaxf(a, b); });
         } else {
+            // a centre outside the image: the reference reads the stage values at the
+            // clamped centre, whose window lies inside the pre-clamped regions
 #pragma unroll
-            for (int j = 0; j < kGfRun; ++j) {
-                const int cx = clampi(ix0 + j, 0, W1), cy = clampi(iy, H0, H1);
+            for (int j = 0; j < kGfV2; ++j) {
+                const int hrow = clampi(iy0 + j, H0, H1) - (y0 - 2 * R);  // H / MR row of the centre
+                const int hcol = clampi(ix, 0, W1) - (x0 - R);            // H column; MR column hcol + R
+                uint32_t a0 = 0, a1 = 0, a2 = 0, am = 0;
+                float mm = 0.f, ms = 0.f;
                 for (int ky = -R; ky <= R; ++ky) {
-                    const uint32_t* xrow = XR + (cy + ky - yr0) * G::XW + (cx - xr0);
-                    const float* mrow = MR + (cy + ky - mr0y) * G::MW + (cx - mr0x);
+                    const int hi_ = (hrow + ky) * G::HWP + hcol;
+                    const uint32_t rbv = H[hi_];
+                    if constexpr (PACKRB) {
+                        a0 += rbv;
+                    } else {
+                        a0 += rbv & 0xffffu;
+                        a2 += rbv >> 16;
+                    }
+                    a1 += H[G::HPL + hi_];
+                    am = pk_max_u16(am, H[2 * G::HPL + hi_]);
+                    const float* mrow = MR + (hrow + ky) * G::MW + hcol;
 #pragma unroll
-                    for (int kx = -R; kx <= R; ++kx) {
-                        const uint32_t p = xrow[kx];
-                        if constexpr (PACKRB) {
-                            s0[j] += p & 0x00ff00ffu;  // R | B<<16 in 16-bit lanes
-                        } else {
-                            s0[j] += p & 0xffu;
-                            s2[j] += __builtin_amdgcn_ubfe(p, 16, 8);
-                        }
-                        s1[j] += __builtin_amdgcn_ubfe(p, 8, 8);
-                        const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);
-                        smax[j] = sb > smax[j] ? sb : smax[j];
-                        smin[j] = sb < smin[j] ? sb : smin[j];
-                        const float m = mrow[kx];
-                        mmax[j] = __builtin_fmaxf(mmax[j], m);
-                        msum[j] = msum[j] + m;
+                    for (int kx = 0; kx < K; ++kx) {
+                        mm = __builtin_fmaxf(mm, mrow[kx]);
+                        ms = ms + mrow[kx];
                     }
                 }
+                s0[j] = a0;
+                s1[j] = a1;
+                s2[j] = a2;
+                smx[j] = am;
+                mmax[j] = mm;
+                msum[j] = ms;
             }
         }
 #pragma unroll
-        for (int j = 0; j < kGfRun; ++j) {
-            const int i = py * G::BW + px0 + j;
-            BR[i] = (float)(PACKRB ? (s0[j] & 0xffffu) : s0[j]) / kk;
-            BR[G::BW * G::BH + i] = (float)s1[j] / kk;
-            BR[2 * G::BW * G::BH + i] = (float)(PACKRB ? (s0[j] >> 16) : s2[j]) / kk;
-            const float imax = (float)(int)smax[j] / 3.f, imin = (float)(int)smin[j] / 3.f;
+        for (int j = 0; j < kGfV2; ++j) {
+            const uint32_t c0 = PACKRB ? (s0[j] & 0xffffu) : s0[j];
+            const uint32_t c2 = PACKRB ? (s0[j] >> 16) : s2[j];
+            res[it][j][0] = div_exact(c0, kk, rkk);
+            res[it][j][1] = div_exact(s1[j], kk, rkk);
+            res[it][j][2] = div_exact(c2, kk, rkk);
+            const float imax = div_exact(smx[j] & 0xffffu, 3.f, kThird);
+            const float imin = div_exact(1023u - (smx[j] >> 16), 3.f, kThird);
             const float num = (imax - imin) * mmax[j];
-            RR[i] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+            res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+        }
+    }
+    __syncthreads();  // H and XR are consumed: BR/RR may overwrite them
+#pragma unroll
+    for (int it = 0; it < G::IT2; ++it) {
+        const int run = tid + it * kGfNT;
+        if (G::NR2 % kGfNT != 0 && run >= G::NR2) continue;
+        const int c = run % G::BW, p0 = (run / G::BW) * kGfV2;
+#pragma unroll
+        for (int j = 0; j < kGfV2; ++j) {
+            const int i = (p0 + j) * G::BW + c;
+            BR[i] = res[it][j][0];
+            BR[G::BPL + i] = res[it][j][1];
+            BR[2 * G::BPL + i] = res[it][j][2];
+            RR[i] = res[it][j][3];
         }
     }
     __syncthreads();
@@ -460,7 +601,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
             uint8_t* g = guide + ((long long)y * width + x) * 3;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
-                const float bm = BR[c * G::BW * G::BH + mi], bc = BR[c * G::BW * G::BH + ci];
+                const float bm = BR[c * G::BPL + mi], bc = BR[c * G::BPL + ci];
                 const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
                 g[c] = (uint8_t)clampi((int)v, 0, 255);
             }
