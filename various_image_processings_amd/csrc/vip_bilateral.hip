@@ -30,9 +30,9 @@ __device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
 #define VIP_STAMP(t, k)
 #endif
 
-template <int R, int WAVES, bool JOINT, bool FMA, int COPIES>
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
-    using G = Geom<R>;
+    using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
     constexpr int TH = WAVES * 4;
     constexpr int ROWS = TH + 2 * R;
@@ -52,10 +52,10 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
 
     // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
     int tile = blockIdx.x;
-    TilePrefetch<R, ROWS, NT> pg, ps;
+    TilePrefetch<R, ROWS, NT, P> pg, ps;
     {
         const int mt = xcd_tile(tile, a.tiles_total);
-        const int tx0 = (mt % a.tiles_x) * kTW, ty0 = (mt / a.tiles_x) * TH;
+        const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
         pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
@@ -67,35 +67,37 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     for ([[maybe_unused]] int it = 0;; ++it) {
         VIP_STAMP(it, 0);
         const int mt = xcd_tile(tile, a.tiles_total);
-        const int tx0 = (mt % a.tiles_x) * kTW, ty0 = (mt / a.tiles_x) * TH;
+        const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
         if (next < a.tiles_total) {  // next tile's HBM reads fly under this tile's taps
             const int mn = xcd_tile(next, a.tiles_total);
-            const int nx0 = (mn % a.tiles_x) * kTW, ny0 = (mn / a.tiles_x) * TH;
+            const int nx0 = (mn % a.tiles_x) * G::TW, ny0 = (mn / a.tiles_x) * TH;
             pg.issue(a.guide, a.guide_pitch, a, nx0, ny0);
             if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
         }
         if (ty0 + wave * 4 < a.out_rows) {  // wave-uniform: skip rows past the frame
-            uint32_t ctr[kP];  // centre pixels of the guide (== src for the plain filter)
+            uint32_t ctr[P];  // centre pixels of the guide (== src for the plain filter)
             {
-                const uint4* c = reinterpret_cast<const uint4*>(gplane + (ty + R) * G::S + tx * kP + G::L);
-                const uint4 c0 = c[0], c1 = c[1];
-                ctr[0] = c0.x; ctr[1] = c0.y; ctr[2] = c0.z; ctr[3] = c0.w;
-                ctr[4] = c1.x; ctr[5] = c1.y; ctr[6] = c1.z; ctr[7] = c1.w;
-            }
-            f2 a01[kP], a2k[kP];  // {sum_b, sum_g}, {sum_r, sumk}
+                const uint4* c = reinterpret_cast<const uint4*>(gplane + (ty + R) * G::S + tx * P + G::L);
 #pragma unroll
-for (int i = 0; i < kP; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
+                for (int q = 0; q < P / 4; ++q) {
+                    const uint4 v = c[q];
+                    ctr[4 * q + 0] = v.x; ctr[4 * q + 1] = v.y; ctr[4 * q + 2] = v.z; ctr[4 * q + 3] = v.w;
+                }
+            }
+            f2 a01[P], a2k[P];  // {sum_b, sum_g}, {sum_r, sumk}
+#pragma unroll
+            for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
             for (int ky = -R; ky <= R; ++ky) {
                 const int aky = ky < 0 ? -ky : ky;
                 const int hw = circle_hw(R, aky);
                 set_progress_priority((ky + R) * 4 / (2 * R + 1));
-                const int row_off = (ty + R + ky) * G::S + tx * kP;
+                const int row_off = (ty + R + ky) * G::S + tx * P;
                 const float* const ws = a.ws + aky * kWsStride;
                 HwDispatch<R, 0>::run(hw, [&](auto hwc) {
                     constexpr int HW = decltype(hwc)::value;
-                    constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + kP - 1 + HW) / 4;
+                    constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + P - 1 + HW) / 4;
                     constexpr int NC = C1 - C0 + 1;
                     uint32_t gp[4 * NC];
                     uint32_t sp[4 * NC];
@@ -113,13 +115,13 @@ for (int i = 0; i < kP; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
                     auto widx = [&](uint32_t g, f2, f2, int i) {
                         return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << (COPIES == 32 ? 7 : 6)) | lane4;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA, false, kP>(gp, sp, wsv, lut_bytes, widx, a01, a2k);
+                    row_taps<HW, G::L, C0, 4 * NC, FMA, false, P>(gp, sp, wsv, lut_bytes, widx, a01, a2k);
                 });
             }
 
-            uint32_t o[kP];
-finish_outputs(a01, a2k, o);
-            store_px(a, ty0 + ty, tx0 + tx * kP, o);
+            uint32_t o[P];
+            finish_outputs(a01, a2k, o);
+            store_px(a, ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);
         if (next >= a.tiles_total) break;
@@ -141,10 +143,21 @@ finish_outputs(a01, a2k, o);
 #ifndef VIP_JBF_MAXW
 #define VIP_JBF_MAXW 16
 #endif
+// Outputs per thread: 8 for the plain filter; the joint filter's second plane and
+// prefetch registers push P = 8 past 128 VGPRs (spills), so it takes 4 by default.
+#ifndef VIP_JBF_P
+#define VIP_JBF_P 4
+#endif
+#ifndef VIP_BIL_P
+#define VIP_BIL_P 8
+#endif
+template <int R, int PLANES>
+constexpr int outputs_per_thread() { return PLANES == 2 ? VIP_JBF_P : VIP_BIL_P; }
 template <int R, int PLANES>
 constexpr int lut_copies() {
+    constexpr int P = outputs_per_thread<R, PLANES>();
     if (!VIP_JBF_LUT16 || PLANES == 1) return 32;
-    return pick_waves<R, PLANES, VIP_JBF_MAXW, 768 * 16>() > pick_waves<R, PLANES>() ? 16 : 32;
+    return pick_waves<R, PLANES, VIP_JBF_MAXW, 768 * 16, P>() > pick_waves<R, PLANES, 16, 768 * 32, P>() ? 16 : 32;
 }
 template <int R, int PLANES>
 constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
@@ -152,12 +165,13 @@ constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
+    constexpr int P = outputs_per_thread<R, PLANES>();
     constexpr int COPIES = lut_copies<R, PLANES>();
-    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), 768 * COPIES>();
+    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), 768 * COPIES, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, PLANES, 768 * COPIES>();
-    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES>;
+    constexpr int LDS = lds_bytes<R, WAVES, PLANES, 768 * COPIES, P>();
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P>;
     static bool attr_done = false;  // benign race: idempotent attribute set
     if (!attr_done) {
         VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -165,7 +179,8 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
         attr_done = true;
     }
     StencilArgs args = a;
-    args.tiles_total = a.tiles_x * ((a.out_rows + TH - 1) / TH);
+    args.tiles_x = (a.width + Geom<R, P>::TW - 1) / Geom<R, P>::TW;
+    args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
