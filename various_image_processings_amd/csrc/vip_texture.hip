@@ -360,22 +360,40 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     const int mr0x = x0 - 2 * R, mr0y = y0 - 2 * R;
     const int W1 = width - 1, H0 = lo, H1 = hi - 1;
 
-    // 1. XR: 4-pixel groups, dword loads when interior and aligned, clamped bytes otherwise
-    for (int g = tid; g < G::XH * (G::XW / 4); g += kGfNT) {
-        const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
-        const uint8_t* row = img + (long long)clampi(yr0 + ry, H0, H1) * width * 3;
-        const int x = xr0 + 4 * gx;
-        uint4 q;
-        if (aligned && x >= 0 && x + 3 <= W1) {
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
-            q = unpack_rgb4(w[0], w[1], w[2]);
-        } else {
-            q.x = load_rgb(row, clampi(x, 0, W1));
-            q.y = load_rgb(row, clampi(x + 1, 0, W1));
-            q.z = load_rgb(row, clampi(x + 2, 0, W1));
-            q.w = load_rgb(row, clampi(x + 3, 0, W1));
+    // 1. XR: 4-pixel groups, dword loads when interior and aligned, clamped bytes
+    //    otherwise; every load of the thread is issued before the first is unpacked
+    //    (one HBM latency per tile, not one per group)
+    {
+        constexpr int NG = G::XH * (G::XW / 4);
+        constexpr int KG = (NG + kGfNT - 1) / kGfNT;
+        uint32_t raw[KG][3];
+#pragma unroll
+        for (int k = 0; k < KG; ++k) {
+            const int g = tid + k * kGfNT;
+            if (NG % kGfNT != 0 && g >= NG) continue;
+            const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
+            const uint8_t* row = img + (long long)clampi(yr0 + ry, H0, H1) * width * 3;
+            const int x = xr0 + 4 * gx;
+            if ((aligned & 1) && x >= 0 && x + 3 <= W1) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
+                raw[k][0] = w[0];
+                raw[k][1] = w[1];
+                raw[k][2] = w[2];
+            } else {
+                const uint32_t q0 = load_rgb(row, clampi(x, 0, W1)), q1 = load_rgb(row, clampi(x + 1, 0, W1));
+                const uint32_t q2 = load_rgb(row, clampi(x + 2, 0, W1)), q3 = load_rgb(row, clampi(x + 3, 0, W1));
+                raw[k][0] = q0 | (q1 << 24);
+                raw[k][1] = (q1 >> 8) | (q2 << 16);
+                raw[k][2] = (q2 >> 16) | (q3 << 8);
+            }
         }
-        *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = q;
+#pragma unroll
+        for (int k = 0; k < KG; ++k) {
+            const int g = tid + k * kGfNT;
+            if (NG % kGfNT != 0 && g >= NG) continue;
+            const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
+            *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = unpack_rgb4(raw[k][0], raw[k][1], raw[k][2]);
+        }
     }
     __syncthreads();
 
@@ -468,8 +486,6 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
             win_sum<kGfV2, K>(hg, s1);
             win_op<kGfV2, K>(hmx, smx, pk_max_u16);
 #pragma unroll
-            for (int j = 0; j < kGfV2; ++j) msum[j] = 0.f;
-#pragma unroll
             for (int t = 0; t < NV; ++t) {
                 const float* mrow = MR + (p0 + t) * G::MW + c;
                 float m[K];
@@ -483,8 +499,10 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 #pragma unroll
                 for (int j = 0; j < kGfV2; ++j) {
                     if (t - j < 0 || t - j >= K) continue;
+                    // the reference starts from 0.f; magnitudes are >= +0, so 0.f + m == m
+                    msum[j] = t == j ? m[0] : msum[j] + m[0];
 #pragma unroll
-                    for (int kx = 0; kx < K; ++kx) msum[j] = msum[j] + m[kx];
+                    for (int kx = 1; kx < K; ++kx) msum[j] = msum[j] + m[kx];
                 }
             }
             win_op<kGfV2, K>(rowmax, mmax, [](float a, float b) { return __builtin_fmaxf(a, b); });
@@ -559,6 +577,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //    found once and shared; scanning those rows in order with strict > then
     //    gives the row-major first argmin. Alpha blend per output.
     const float sigma_alpha = 1.f / (float)(5 * ksize);
+    uint32_t* GT = reinterpret_cast<uint32_t*>(MR);  // guide tile as RGBX words (MR is consumed)
+    static_assert(kGfTW * kGfTH <= G::MW * G::MH, "guide tile does not fit the MR region");
     for (int run = tid; run < (kGfTH / kGfRun) * kGfTW; run += kGfNT) {
         const int tx = run % kGfTW, ty0 = (run / kGfTW) * kGfRun;
         const int x = x0 + tx;
@@ -598,12 +618,39 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
             const float e = (float)exp((double)arg);
             const float alpha = 2.f / (1.f + e) - 1.f;
             const float beta = 1.f - alpha;
-            uint8_t* g = guide + ((long long)y * width + x) * 3;
+            uint32_t gw = 0;
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 const float bm = BR[c * G::BPL + mi], bc = BR[c * G::BPL + ci];
                 const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
-                g[c] = (uint8_t)clampi((int)v, 0, 255);
+                gw |= (uint32_t)clampi((int)v, 0, 255) << (8 * c);
+            }
+            GT[(ty0 + j) * kGfTW + tx] = gw;
+        }
+    }
+    __syncthreads();
+
+    // 5. guide tile -> HBM: 4 RGBX words -> 3 dwords per thread (byte stores at a
+    //    ragged right edge or an unaligned buffer)
+    for (int q = tid; q < kGfTH * (kGfTW / 4); q += kGfNT) {
+        const int gr = q / (kGfTW / 4), x = x0 + 4 * (q - gr * (kGfTW / 4));
+        const int y = y0 + gr;
+        if (y >= gy1 || x > W1) continue;
+        const uint4 w = *reinterpret_cast<const uint4*>(GT + gr * kGfTW + (x - x0));
+        uint8_t* row = guide + ((long long)y * width + x) * 3;
+        if ((aligned & 2) && x + 3 <= W1) {
+            uint32_t* d = reinterpret_cast<uint32_t*>(row);
+            d[0] = w.x | (w.y << 24);
+            d[1] = (w.y >> 8) | (w.z << 16);
+            d[2] = (w.z >> 16) | (w.w << 8);
+        } else {
+            const uint32_t ws_[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (x + i > W1) break;
+                row[3 * i] = (uint8_t)ws_[i];
+                row[3 * i + 1] = (uint8_t)(ws_[i] >> 8);
+                row[3 * i + 2] = (uint8_t)(ws_[i] >> 16);
             }
         }
     }
@@ -645,7 +692,9 @@ static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width,
 
 int launch_texture_guide_fused_rows(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
                                     int ksize, bool cpp, hipStream_t stream) {
-    const int aligned = ((uintptr_t)img % 4 == 0) && ((size_t)width * 3 % 4 == 0);
+    // bit 0: image rows dword-aligned (dword tile loads); bit 1: guide rows (dword stores)
+    const int aligned = (((uintptr_t)img % 4 == 0) && ((size_t)width * 3 % 4 == 0) ? 1 : 0) |
+                        (((uintptr_t)guide % 4 == 0) && ((size_t)width * 3 % 4 == 0) ? 2 : 0);
     return cpp ? launch_gf_r<true>(ksize, img, guide, width, lo, hi, gy0, gy1, aligned, stream)
                : launch_gf_r<false>(ksize, img, guide, width, lo, hi, gy0, gy1, aligned, stream);
 }
