@@ -155,8 +155,6 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     constexpr int HW = decltype(hwc)::value;
                     constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + P - 1 + HW) / 4;
                     constexpr int NC = C1 - C0 + 1;
-                    uint32_t gp[4 * NC];
-                    load_row<C0, NC>(plane, row_off, gp);
                     float wsv[HW + 1];
         #pragma unroll
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
@@ -170,7 +168,8 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                         const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
                         return ((uint32_t)dist << 6) | lane16;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA, true, P>(gp, gp, wsv, lut_bytes, widx, a01, a2k);
+                    row_taps<HW, G::L, C0, NC, FMA, true, P, false>(plane, plane, row_off, wsv, lut_bytes, widx, a01,
+                                                                    a2k);
                 });
             }
 

@@ -99,15 +99,6 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                     constexpr int HW = decltype(hwc)::value;
                     constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + P - 1 + HW) / 4;
                     constexpr int NC = C1 - C0 + 1;
-                    uint32_t gp[4 * NC];
-                    uint32_t sp[4 * NC];
-                    load_row<C0, NC>(gplane, row_off, gp);
-                    if constexpr (JOINT) {
-                        load_row<C0, NC>(splane, row_off, sp);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 4 * NC; ++q) sp[q] = gp[q];
-                    }
                     float wsv[HW + 1];
 #pragma unroll
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
@@ -115,7 +106,8 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                     auto widx = [&](uint32_t g, f2, f2, int i) {
                         return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << (COPIES == 32 ? 7 : 6)) | lane4;
                     };
-                    row_taps<HW, G::L, C0, 4 * NC, FMA, false, P>(gp, sp, wsv, lut_bytes, widx, a01, a2k);
+                    row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT>(gplane, splane, row_off, wsv, lut_bytes, widx,
+                                                                     a01, a2k);
                 });
             }
 

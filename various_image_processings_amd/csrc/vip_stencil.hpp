@@ -202,22 +202,37 @@ __device__ __forceinline__ void stage_lut(uint32_t* lut, const float* color) {
     }
 }
 
-// Load the 4*NC neighbour words of columns [4*C0, 4*C0 + 4*NC) of one tile row
-// (row_off is 16-byte aligned; indexing as uint4 lets hipcc emit ds_read_b128).
-template <int C0, int NC>
-__device__ __forceinline__ void load_row(const uint32_t* plane, int row_off, uint32_t (&w)[4 * NC]) {
+// Neighbour words of one tile row, columns [4*C0, 4*C0 + 4*NC), read from LDS in
+// 4-word chunks (row_off is 16-byte aligned; indexing as uint4 gives ds_read_b128).
+// row_taps loads a chunk only a few columns before its first use, so just a short
+// window of the row is live in registers (the whole row of a large radius is not:
+// 40 words per plane at R = 15, which spilled).
+template <int C0, int NC, bool TWO>
+struct RowStream {
     // volatile: keep every load a full ds_read_b128 (hipcc otherwise narrows the
     // edge chunks to the words the row uses and re-pairs them as misaligned,
     // bank-conflicting ds_read2_b32)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     typedef __attribute__((address_space(3))) const volatile u32x4 lds_u32x4;
-    lds_u32x4* v = (lds_u32x4*)(plane) + (row_off >> 2) + C0;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const u32x4 q = v[c];
-        w[4 * c + 0] = q.x; w[4 * c + 1] = q.y; w[4 * c + 2] = q.z; w[4 * c + 3] = q.w;
+    lds_u32x4* g;
+    lds_u32x4* s;
+    uint32_t gw[4 * NC], sw[4 * NC];
+
+    __device__ __forceinline__ RowStream(const uint32_t* gplane, const uint32_t* splane, int row_off)
+        : g((lds_u32x4*)(gplane) + (row_off >> 2) + C0), s((lds_u32x4*)(splane) + (row_off >> 2) + C0) {}
+
+    __device__ __forceinline__ void load(int q) {
+        const u32x4 v = g[q];
+        gw[4 * q + 0] = v.x; gw[4 * q + 1] = v.y; gw[4 * q + 2] = v.z; gw[4 * q + 3] = v.w;
+        if constexpr (TWO) {
+            const u32x4 u = s[q];
+            sw[4 * q + 0] = u.x; sw[4 * q + 1] = u.y; sw[4 * q + 2] = u.z; sw[4 * q + 3] = u.w;
+        }
     }
-}
+    // word k (relative to column 4*C0) of the guide / source plane
+    __device__ __forceinline__ uint32_t guide(int k) const { return gw[k]; }
+    __device__ __forceinline__ uint32_t source(int k) const { return TWO ? sw[k] : gw[k]; }
+};
 
 // Progress-based wave priority. The SIMD arbiter serves ready waves by priority,
 // then age, so with equal priorities the oldest wave of each SIMD races through
@@ -256,19 +271,30 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 // PK: accumulate with v_pk_fma_f32 ({s0,s1} and {s2,sk} pairs). Measured on gfx950:
 // +3 % for the adaptive kernel, -10 % for the bilateral kernel (the {r, 1} pairs
 // push it past 128 VGPRs), so it is a per-kernel choice.
-template <int HW, int L, int C0, int NGP, bool FMA, bool PK, int P, class WIdx>
-__device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32_t (&sp)[NGP],
+// TWO: separate guide and source planes (joint bilateral); otherwise one plane.
+#ifndef VIP_ROW_LOOKAHEAD
+#define VIP_ROW_LOOKAHEAD 4  // columns between a chunk's LDS read and its first use
+#endif
+template <int HW, int L, int C0, int NC, bool FMA, bool PK, int P, bool TWO, class WIdx>
+__device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t* splane, int row_off,
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
                                          f2 (&a01)[P], f2 (&a2k)[P]) {
     constexpr int D = VIP_PIPE_DEPTH;
     constexpr int NB = D + 1;            // ring of in-flight columns
     constexpr int J0 = L - HW;           // first neighbour column relative to the thread's P
     constexpr int J1 = L + P - 1 + HW;   // last
+    constexpr int LA = D + VIP_ROW_LOOKAHEAD;
+    static_assert(J0 >= 4 * C0 && J1 < 4 * (C0 + NC), "row chunk range");
+    auto chunk = [](int j) constexpr { return (j - 4 * C0) >> 2; };
+    constexpr int PRE = chunk(J0 + LA < J1 ? J0 + LA : J1);  // chunks read before the loop
+    RowStream<C0, NC, TWO> row(gplane, splane, row_off);
+#pragma unroll
+    for (int q = 0; q <= PRE; ++q) row.load(q);
     float wc[NB][P];
     f2 n01[NB], n21[NB];                 // {b, g} and {r, 1} of the neighbour (source image)
     auto issue = [&](int j) {
-        const uint32_t g = gp[j - 4 * C0];
-        const uint32_t p = sp[j - 4 * C0];
+        const uint32_t g = row.guide(j - 4 * C0);
+        const uint32_t p = row.source(j - 4 * C0);
         const int b = (j - J0) % NB;
         n01[b].x = (float)(p & 0xffu);
         n01[b].y = (float)((p >> 8) & 0xffu);
@@ -285,6 +311,7 @@ __device__ __forceinline__ void row_taps(const uint32_t (&gp)[NGP], const uint32
     for (int j = J0; j < J0 + D && j <= J1; ++j) issue(j);
 #pragma unroll
     for (int j = J0; j <= J1; ++j) {
+        if (j + LA <= J1 && ((j + LA) & 3) == 0 && chunk(j + LA) > PRE) row.load(chunk(j + LA));
         if (j + D <= J1) issue(j + D);
         const int b = (j - J0) % NB;
 #pragma unroll
