@@ -252,8 +252,8 @@ def main():
         # blur_rtv 7+16, guide 16+3, JBF 6+3 = 58 B
         bytes_launch = 58.0 * px_per_rank * cfg["nitr"]
         achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = pmc_traffic(args.config, ["void vip::texture_guide_fused_kernel", "void vip::bilateral_kernel"],
-                                    cfg["nitr"])
+        traffic, tsrc = (None, None) if world > 1 else pmc_traffic(
+            args.config, ["void vip::texture_guide_fused_kernel", "void vip::bilateral_kernel"], cfg["nitr"])
         roof = dict(bound="hbm", achieved=round(achieved, 2), peak=PEAK_HBM_GBS, unit="GB/s",
                     frac=round(achieved / PEAK_HBM_GBS, 4), traffic=traffic, traffic_source=tsrc,
                     kernel="whole texture pipeline per launch (gradient, blur_rtv, guide, JBF) x nitr",
@@ -263,8 +263,8 @@ def main():
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
         tflops = flops / (kernel_ms * 1e-3) / 1e12
         hbm = 6.0 * px_per_rank / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = (None, None) if world > 1 or "frame_height" in cfg else \
-            pmc_traffic(args.config, [f"void vip::{cfg['kind']}_kernel<{r},"])
+        # the committed PMC summaries are single-GPU whole-frame launches
+        traffic, tsrc = (None, None) if world > 1 else pmc_traffic(args.config, [f"void vip::{cfg['kind']}_kernel<{r},"])
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
