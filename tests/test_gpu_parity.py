@@ -94,6 +94,20 @@ def test_adaptive(dev, oracle, k, numerics, profile):
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
+@pytest.mark.parametrize("k", [5, 15, 17, 19])
+def test_adaptive_multi_tile(dev, oracle, k):
+    # several persistent tiles per workgroup, ragged edges; k <= 17 takes the separable
+    # box-sum path (17: R|B sums unpacked before the horizontal windows), 19 the
+    # per-thread square sums
+    img = oracle.random_image(701, 331)
+    h, w, _ = img.shape
+    f = vip.CudaAdaptiveBilateralFilter(w, h, k)
+    d_dst = dev.empty((h, w, 3))
+    f.execute(dev.put(img), d_dst)
+    got, want = dev.get(d_dst), oracle.adaptive(img, k, threads=16)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
 def test_adaptive_natural_image(dev, oracle, lenna):
     h, w, _ = lenna.shape
     f = vip.CudaAdaptiveBilateralFilter(w, h, 15)

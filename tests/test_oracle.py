@@ -186,12 +186,14 @@ def _fma32(a, b, c):
 
 @pytest.mark.skipif(np.finfo(np.longdouble).nmant < 63, reason="needs x87 80-bit long double")
 def test_constant_division_is_exact():
-    """The fused texture guide stage (vip_texture.hip div_exact) divides the integer
-    box sums by ksize^2 and the intensity byte sums by 3 with an fma-corrected
-    reciprocal: q0 = s*rd, q = fma(fma(-q0, d, s), rd, q0). It must equal the correctly
-    rounded float quotient the reference computes (src/bilateral_texture_filter_impl.cu:
-    97-100, :84) for EVERY reachable numerator -- checked exhaustively here."""
-    cases = [((2 * (k // 2) + 1) ** 2 * 255, k * k) for k in range(2, 18)] + [(765, 3)]
+    """The fused texture guide stage and the adaptive kernel (vip_stencil.hpp
+    div_exact) divide integer box sums by ksize^2, and intensity byte sums by 3, with
+    an fma-corrected reciprocal: q0 = s*rd, q = fma(fma(-q0, d, s), rd, q0). It must
+    equal the correctly rounded float quotient the reference computes
+    (src/bilateral_texture_filter_impl.cu:97-100, :84;
+    src/adaptive_bilateral_filter_impl.cu:88-92) for EVERY reachable numerator --
+    checked exhaustively here (texture ksize 2..17, adaptive ksize up to 31)."""
+    cases = [((2 * (k // 2) + 1) ** 2 * 255, k * k) for k in range(2, 32)] + [(765, 3)]
     for smax, d in cases:
         s = np.arange(smax + 1, dtype=np.float32)
         d32 = np.float32(d)

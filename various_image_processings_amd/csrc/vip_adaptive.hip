@@ -19,6 +19,16 @@
 
 namespace vip {
 
+// Separable box sums need VRB (TH x VW words) after the plane and VW u16 of VG in each
+// plane row's unused tail (S - VW words): true up to R = 8 at 16 waves.
+template <int R, int P, int WAVES>
+constexpr bool adaptive_vbox() {
+    using G = Geom<R, P>;
+    constexpr int VW = G::GROUPS * 4;
+    return VW <= 2 * (G::S - VW) &&
+           lds_bytes<R, WAVES, 1, lut_words(true), P>() + 4LL * (WAVES * 4) * VW <= kLdsBudget;
+}
+
 template <int R, int WAVES, bool FMA, int P>
 __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
@@ -30,9 +40,16 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     constexpr int NCOL = P + 2 * R;            // columns touched by the thread's P windows
     constexpr int JB = G::L - R;               // first column relative to tx*P
     constexpr int CB0 = JB / 4, CB1 = (G::L + P - 1 + R) / 4;
+    // VBOX: the k x k box sums are separable -- vertical K-row sums of the tile plane
+    // are computed once per tile cooperatively (VRB: R|B<<16 per column, VG: G as u16 in
+    // the plane rows' unused tail words), then each thread slides its K-column windows
+    // over them. Fits the LDS for R <= 8; larger radii keep the per-thread square sums.
+    constexpr int VW = G::GROUPS * 4;          // plane words in use per row (TW + 2L)
+    constexpr bool VBOX = adaptive_vbox<R, P, WAVES>();
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
     uint32_t* const plane = lds + lut_words(true);
+    uint32_t* const vrb = plane + ROWS * G::S;  // VBOX: TH x VW words
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -60,7 +77,97 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
             const int mn = xcd_tile(next, a.tiles_total);
             pf.issue(a.src, a.src_pitch, a, (mn % a.tiles_x) * G::TW, (mn / a.tiles_x) * TH);
         }
+        if constexpr (VBOX) {
+            // ---- pass 1a (whole workgroup): vertical K-row sums, 4 output rows per run ----
+            // output row r <-> plane rows r .. r + 2R; every sum is an exact integer
+            for (int run = tid; run < VW * (TH / 4); run += NT) {
+                const int c = run % VW, r0 = (run / VW) * 4;
+                uint32_t rb[4 + K - 1], gg[4 + K - 1], orb[4], og[4];
+        #pragma unroll
+                for (int t = 0; t < 4 + K - 1; ++t) {
+                    const uint32_t p = plane[(r0 + t) * G::S + c];
+                    rb[t] = p & 0x00ff00ffu;            // K * 255 per 16-bit field
+                    gg[t] = __builtin_amdgcn_ubfe(p, 8, 8);
+                }
+                win_sum<4, K>(rb, orb);
+                win_sum<4, K>(gg, og);
+        #pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    vrb[(r0 + j) * VW + c] = orb[j];
+                    reinterpret_cast<uint16_t*>(plane + (r0 + j) * G::S + VW)[c] = (uint16_t)og[j];
+                }
+            }
+            __syncthreads();
+        }
         if (ty0 + wave * 4 < a.out_rows) {
+            uint32_t ctr[P];
+            {
+                const uint4* c = reinterpret_cast<const uint4*>(plane + (ty + R) * G::S + tx * P + G::L);
+        #pragma unroll
+                for (int q = 0; q < P / 4; ++q) {
+                    const uint4 v = c[q];
+                    ctr[4 * q + 0] = v.x; ctr[4 * q + 1] = v.y; ctr[4 * q + 2] = v.z; ctr[4 * q + 3] = v.w;
+                }
+            }
+            float c0f[P], c1f[P], c2f[P], o0[P], o1[P], o2[P];
+            const float kk = (float)(K * K);
+            const float rkk = 1.f / kk;
+            // offset = centre - box mean, as the reference (src/adaptive_bilateral_filter_impl.cu:88-92)
+            auto set_offsets = [&](int i, uint32_t sr, uint32_t sg, uint32_t sb) {
+                c0f[i] = (float)(ctr[i] & 0xffu);
+                c1f[i] = (float)((ctr[i] >> 8) & 0xffu);
+                c2f[i] = (float)((ctr[i] >> 16) & 0xffu);
+                // opaque to the optimiser: otherwise fsub(uitofp n, uitofp c) in the tap
+                // loop is rewritten as an integer v_sub_u32_sdwa + v_cvt_f32_i32 per
+                // channel and pair (two slow ops instead of one v_sub_f32)
+                __asm__("" : "+v"(c0f[i]), "+v"(c1f[i]), "+v"(c2f[i]));
+                o0[i] = c0f[i] - div_exact(sr, kk, rkk);
+                o1[i] = c1f[i] - div_exact(sg, kk, rkk);
+                o2[i] = c2f[i] - div_exact(sb, kk, rkk);
+            };
+            if constexpr (VBOX) {
+                // ---- pass 1b (per thread): K-column windows of the vertical sums ----
+                constexpr int NCOLV = P + K - 1;
+                uint32_t hrb[NCOLV], hg[NCOLV];
+                const uint32_t* vrow = vrb + ty * VW + tx * P;
+                const uint16_t* grow = reinterpret_cast<const uint16_t*>(plane + ty * G::S + VW) + tx * P;
+        #pragma unroll
+                for (int c = CB0; c <= CB1; ++c) {
+                    const uint4 q4 = *reinterpret_cast<const uint4*>(vrow + 4 * c);
+                    const uint2 g2 = *reinterpret_cast<const uint2*>(grow + 4 * c);
+                    const uint32_t w4[4] = {q4.x, q4.y, q4.z, q4.w};
+                    const uint32_t g4[4] = {g2.x & 0xffffu, g2.x >> 16, g2.y & 0xffffu, g2.y >> 16};
+        #pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const int j = 4 * c + t - JB;
+                        if (j < 0 || j >= NCOLV) continue;
+                        hrb[j] = w4[t];
+                        hg[j] = g4[t];
+                    }
+                }
+                uint32_t wg[P], wr[P], wb[P];
+                win_sum<P, K>(hg, wg);
+                if constexpr (PACK) {
+                    uint32_t wrb[P];
+                    win_sum<P, K>(hrb, wrb);
+        #pragma unroll
+                    for (int i = 0; i < P; ++i) {
+                        wr[i] = wrb[i] & 0xffffu;
+                        wb[i] = wrb[i] >> 16;
+                    }
+                } else {
+                    uint32_t hr[NCOLV], hb[NCOLV];
+        #pragma unroll
+                    for (int t = 0; t < NCOLV; ++t) {
+                        hr[t] = hrb[t] & 0xffffu;
+                        hb[t] = hrb[t] >> 16;
+                    }
+                    win_sum<P, K>(hr, wr);
+                    win_sum<P, K>(hb, wb);
+                }
+        #pragma unroll
+                for (int i = 0; i < P; ++i) set_offsets(i, wr[i], wg[i], wb[i]);
+            } else {
             // ---- pass 1: box sums over the full square ----
             // Column sums are kept only for the columns the sliding window adds or
             // drops (slot j < P-1 and j >= K); the window's other columns go straight
@@ -68,10 +175,10 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
             constexpr int HI0 = (K > P - 1) ? K : P - 1;     // first column with a "hi" slot
             constexpr int NSLOT = (P - 1) + (K + P - 1 - HI0);
             auto slot = [](int j) constexpr { return j < P - 1 ? j : (j >= HI0 ? P - 1 + j - HI0 : -1); };
-            uint32_t vrb[NSLOT], vg[NSLOT], vb[PACK ? 1 : NSLOT];
+            uint32_t vrb_[NSLOT], vg[NSLOT], vb[PACK ? 1 : NSLOT];
             uint32_t mrb = 0u, mg = 0u, mb = 0u;            // columns in [P-1, K) without a slot
         #pragma unroll
-            for (int q = 0; q < NSLOT; ++q) { vrb[q] = 0u; vg[q] = 0u; if constexpr (!PACK) vb[q] = 0u; }
+            for (int q = 0; q < NSLOT; ++q) { vrb_[q] = 0u; vg[q] = 0u; if constexpr (!PACK) vb[q] = 0u; }
             for (int r = 0; r < K; ++r) {
                 const uint32_t* row = plane + (ty + r) * G::S + tx * P;
         #pragma unroll
@@ -84,7 +191,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                         if (j < 0 || j >= NCOL) continue;
                         const uint32_t p = w4[t];
                         const int q = slot(j);
-                        uint32_t& arb = q >= 0 ? vrb[q < 0 ? 0 : q] : mrb;
+                        uint32_t& arb = q >= 0 ? vrb_[q < 0 ? 0 : q] : mrb;
                         uint32_t& ag = q >= 0 ? vg[q < 0 ? 0 : q] : mg;
                         if constexpr (PACK) {
                             arb += p & 0x00ff00ffu;
@@ -98,46 +205,25 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     }
                 }
             }
-            uint32_t ctr[P];
-            float c0f[P], c1f[P], c2f[P], o0[P], o1[P], o2[P];
-            {
-                const uint4* c = reinterpret_cast<const uint4*>(plane + (ty + R) * G::S + tx * P + G::L);
-        #pragma unroll
-                for (int q = 0; q < P / 4; ++q) {
-                    const uint4 v = c[q];
-                    ctr[4 * q + 0] = v.x; ctr[4 * q + 1] = v.y; ctr[4 * q + 2] = v.z; ctr[4 * q + 3] = v.w;
-                }
-            }
             {
                 uint32_t wrb = mrb, wg = mg, wb = mb;
         #pragma unroll
                 for (int j = 0; j < K; ++j) {
                     const int q = slot(j);
                     if (q < 0) continue;
-                    wrb += vrb[q]; wg += vg[q]; if constexpr (!PACK) wb += vb[q];
+                    wrb += vrb_[q]; wg += vg[q]; if constexpr (!PACK) wb += vb[q];
                 }
-                const float kk = (float)(K * K);
         #pragma unroll
                 for (int i = 0; i < P; ++i) {
                     if (i > 0) {
                         const int qa = slot(i + K - 1), qd = slot(i - 1);
-                        wrb += vrb[qa] - vrb[qd];
+                        wrb += vrb_[qa] - vrb_[qd];
                         wg += vg[qa] - vg[qd];
                         if constexpr (!PACK) wb += vb[qa] - vb[qd];
                     }
-                    const uint32_t sr = PACK ? (wrb & 0xffffu) : wrb;
-                    const uint32_t sb = PACK ? (wrb >> 16) : wb;
-                    c0f[i] = (float)(ctr[i] & 0xffu);
-                    c1f[i] = (float)((ctr[i] >> 8) & 0xffu);
-                    c2f[i] = (float)((ctr[i] >> 16) & 0xffu);
-                    // opaque to the optimiser: otherwise fsub(uitofp n, uitofp c) in the tap
-                    // loop is rewritten as an integer v_sub_u32_sdwa + v_cvt_f32_i32 per
-                    // channel and pair (two slow ops instead of one v_sub_f32)
-                    __asm__("" : "+v"(c0f[i]), "+v"(c1f[i]), "+v"(c2f[i]));
-                    o0[i] = c0f[i] - (float)sr / kk;
-                    o1[i] = c1f[i] - (float)wg / kk;
-                    o2[i] = c2f[i] - (float)sb / kk;
+                    set_offsets(i, PACK ? (wrb & 0xffffu) : wrb, wg, PACK ? (wrb >> 16) : wb);
                 }
+            }
             }
 
             // ---- pass 2: offset-weighted bilateral over the disc ----
@@ -194,7 +280,9 @@ static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
     constexpr int WAVES = pick_waves<R, 1, P == 8 ? 8 : 16, lut_words(true), P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, 1, lut_words(true), P>();
+    constexpr int LDS = lds_bytes<R, WAVES, 1, lut_words(true), P>() +
+                        (adaptive_vbox<R, P, WAVES>() ? 4 * TH * G::GROUPS * 4 : 0);
+    static_assert(LDS <= kLdsBudget, "adaptive tile does not fit LDS");
     auto kern = adaptive_kernel<R, WAVES, FMA, P>;
     static bool attr_done = false;
     if (!attr_done) {

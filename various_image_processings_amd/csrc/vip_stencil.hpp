@@ -134,6 +134,30 @@ __device__ __forceinline__ uint32_t load_rgb(const uint8_t* row, int x) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16);
 }
 
+// N sliding sums of K consecutive terms of x (integer: the add/subtract slide is exact)
+template <int N, int K>
+__device__ __forceinline__ void win_sum(const uint32_t (&x)[N + K - 1], uint32_t (&o)[N]) {
+    uint32_t s = x[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) s += x[k];
+    o[0] = s;
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        s = s + x[j + K - 1] - x[j - 1];
+        o[j] = s;
+    }
+}
+
+// Correctly rounded (float)s / d for an integer box sum s and the constant d = k^2
+// (or 3): q0 = s*rd, one fma residual, one fma correction. Equal to the IEEE quotient
+// for every s in [0, k^2 * 255], k <= 31 -- checked exhaustively in
+// tests/test_oracle.py::test_constant_division_is_exact (rd = RN(1/d)).
+__device__ __forceinline__ float div_exact(uint32_t s, float d, float rd) {
+    const float f = (float)s;
+    const float q0 = f * rd;
+    return __builtin_fmaf(__builtin_fmaf(-q0, d, f), rd, q0);
+}
+
 // Register-staged prefetch of one tile plane: source rows
 // [ty0 + src_row0 - R, +ROWS) x columns [tx0 - L, tx0 - L + TW + 2L) of `img`, rows
 // clamped to [row_lo, row_hi), columns to [0, width) (the reference's replicate

@@ -292,20 +292,6 @@ __device__ __forceinline__ uint32_t pk_max_u16(uint32_t a, uint32_t b) {
                                                                   __builtin_bit_cast(gf_u16x2, b)));
 }
 
-// N sliding sums of K consecutive terms of x (integer: the add/subtract slide is exact)
-template <int N, int K>
-__device__ __forceinline__ void win_sum(const uint32_t (&x)[N + K - 1], uint32_t (&o)[N]) {
-    uint32_t s = x[0];
-#pragma unroll
-    for (int k = 1; k < K; ++k) s += x[k];
-    o[0] = s;
-#pragma unroll
-    for (int j = 1; j < N; ++j) {
-        s = s + x[j + K - 1] - x[j - 1];
-        o[j] = s;
-    }
-}
-
 // N sliding maxima (any associative, idempotent op) of K consecutive terms: blocks of
 // K, suffix scans inside a block and prefix scans into the next, window j =
 // op(suffix[j], prefix[j + K - 1]) (van Herk / Gil-Werman).
@@ -325,13 +311,6 @@ __device__ __forceinline__ void win_op(const T (&x)[N + K - 1], T (&o)[N], Op op
     }
 #pragma unroll
     for (int j = 0; j < N; ++j) o[j] = (j % K == 0) ? suf[j] : op(suf[j], pre[j + K - 1]);
-}
-
-// correctly rounded (float)s / d for the reachable integer numerators s (see header)
-__device__ __forceinline__ float div_exact(uint32_t s, float d, float rd) {
-    const float f = (float)s;
-    const float q0 = f * rd;
-    return __builtin_fmaf(__builtin_fmaf(-q0, d, f), rd, q0);
 }
 
 // Row bands: rows [lo, hi) of the (dense, width*3 pitch) buffers are the valid
