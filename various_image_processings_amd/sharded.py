@@ -84,6 +84,26 @@ def exchange_halo(slab, geo: SlabGeometry, group=None) -> None:
     # gloo moves host tensors only: a device slab is staged through host copies
     # (CPU rehearsal of the N>1 path; with nccl = RCCL the slab rows go GPU to GPU)
     staged = slab.is_cuda and dist.get_backend(group) == "gloo"
+    if not staged:
+        # the per-step host work is only the batched launch: the row views and P2P
+        # ops of a slab buffer are built once (bench.py rotates a fixed set of slabs)
+        key = (slab.data_ptr(), tuple(slab.shape), slab.device, group)
+        cache = geo.__dict__.setdefault("_p2p_ops", {})
+        ops = cache.get(key)
+        if ops is None:
+            ops = []
+            if geo.has_above:
+                ops.append(dist.P2POp(dist.isend, slab[r:2 * r], geo.rank - 1, group))
+                ops.append(dist.P2POp(dist.irecv, slab[0:r], geo.rank - 1, group))
+            if geo.has_below:
+                ops.append(dist.P2POp(dist.isend, slab[n:n + r], geo.rank + 1, group))
+                ops.append(dist.P2POp(dist.irecv, slab[n + r:n + 2 * r], geo.rank + 1, group))
+            if len(cache) >= 32:  # the views keep their slabs alive: bound the cache
+                cache.pop(next(iter(cache)))
+            cache[key] = ops
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        return
     sends, recvs = [], []
     if geo.has_above:
         sends.append((slab[r:2 * r], geo.rank - 1))
