@@ -231,14 +231,12 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
         #pragma unroll
             for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
-            for (int ky = -R; ky <= R; ++ky) {
-                const int aky = ky < 0 ? -ky : ky;
-                const int hw = circle_hw(R, aky);
-                set_progress_priority((ky + R) * 4 / (2 * R + 1));
-                const int row_off = (ty + R + ky) * G::S + tx * P;
-                const float* const ws = a.ws + aky * kWsStride;
-                HwDispatch<R, 0>::run(hw, [&](auto hwc) {
+            for_each_row<R, false>([&](const int ky, auto hwc) {
                     constexpr int HW = decltype(hwc)::value;
+                    const int aky = ky < 0 ? -ky : ky;
+                    set_progress_priority((ky + R) * 4 / (2 * R + 1));
+                    const int row_off = (ty + R + ky) * G::S + tx * P;
+                    const float* const ws = a.ws + aky * kWsStride;
                     constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + P - 1 + HW) / 4;
                     constexpr int NC = C1 - C0 + 1;
                     float wsv[HW + 1];
@@ -256,8 +254,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     };
                     row_taps<HW, G::L, C0, NC, FMA, true, P, false>(plane, plane, row_off, wsv, lut_bytes, widx, a01,
                                                                     a2k);
-                });
-            }
+            });
 
             uint32_t o[P];
             finish_outputs(a01, a2k, o);

@@ -30,11 +30,15 @@ __device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
 #define VIP_STAMP(t, k)
 #endif
 
+#ifndef VIP_BIL_UNROLL_MAX_R
+#define VIP_BIL_UNROLL_MAX_R 8
+#endif
 template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
     constexpr int TH = WAVES * 4;
+    constexpr bool ROW_UNROLL = R <= VIP_BIL_UNROLL_MAX_R;  // straight-line rows (for_each_row)
     constexpr int ROWS = TH + 2 * R;
     constexpr int PLANE = ROWS * G::S;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -89,14 +93,12 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
 #pragma unroll
             for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
-            for (int ky = -R; ky <= R; ++ky) {
-                const int aky = ky < 0 ? -ky : ky;
-                const int hw = circle_hw(R, aky);
-                set_progress_priority((ky + R) * 4 / (2 * R + 1));
-                const int row_off = (ty + R + ky) * G::S + tx * P;
-                const float* const ws = a.ws + aky * kWsStride;
-                HwDispatch<R, 0>::run(hw, [&](auto hwc) {
+            for_each_row<R, ROW_UNROLL>([&](const int ky, auto hwc) {
                     constexpr int HW = decltype(hwc)::value;
+                    const int aky = ky < 0 ? -ky : ky;
+                    set_progress_priority((ky + R) * 4 / (2 * R + 1));
+                    const int row_off = (ty + R + ky) * G::S + tx * P;
+                    const float* const ws = a.ws + aky * kWsStride;
                     constexpr int C0 = (G::L - HW) / 4, C1 = (G::L + P - 1 + HW) / 4;
                     constexpr int NC = C1 - C0 + 1;
                     float wsv[HW + 1];
@@ -108,8 +110,8 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                     };
                     row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT>(gplane, splane, row_off, wsv, lut_bytes, widx,
                                                                      a01, a2k);
-                });
-            }
+                    if constexpr (ROW_UNROLL) fence_accumulators(a01, a2k);
+            });
 
             uint32_t o[P];
             finish_outputs(a01, a2k, o);

@@ -13,6 +13,8 @@
 // 8*(l%16) .. 8*(l%16)+7 (P = 8 horizontally adjacent outputs per thread).
 #pragma once
 
+#include <utility>
+
 #include "vip_common.hpp"
 
 namespace vip {
@@ -118,6 +120,29 @@ struct HwDispatch {
         if constexpr (KY < R) HwDispatch<R, KY + 1>::run(hw, static_cast<F&&>(f));
     }
 };
+
+// Runs f(ky, integral_constant<hw>) for the tile rows ky = -R..R, in order.
+// UNROLL: every row is straight-line code with a compile-time half-width, so the
+// accumulators stay in their registers from row to row (the caller fences them at
+// each row end, see fence_accumulators). Otherwise a runtime row loop dispatches to
+// one body per distinct half-width -- half the code, but the register allocator then
+// copies every accumulator at each join (2 x 32 v_mov per row for 8 outputs, found
+// in the ISA). Measured: bilateral r=7 240 -> 226 us, joint r=4 94 -> 85 us unrolled;
+// the adaptive kernel (larger bodies) and r=15 (C5) are faster with the loop.
+template <int R, bool UNROLL, class F>
+__device__ __forceinline__ void for_each_row(F&& f) {
+    if constexpr (UNROLL) {
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+            ((f(I - R, std::integral_constant<int, circle_hw(R, I < R ? R - I : I - R)>{}),
+              __builtin_amdgcn_sched_barrier(0)), ...);
+        }(std::make_integer_sequence<int, 2 * R + 1>{});
+    } else {
+        for (int ky = -R; ky <= R; ++ky) {
+            const int aky = ky < 0 ? -ky : ky;
+            HwDispatch<R, 0>::run(circle_hw(R, aky), [&](auto hwc) { f(ky, hwc); });
+        }
+    }
+}
 
 // 12 bytes (4 RGB pixels) -> 4 RGBX words.
 __device__ __forceinline__ uint4 unpack_rgb4(uint32_t a, uint32_t b, uint32_t c) {
@@ -291,6 +316,15 @@ __device__ __forceinline__ void set_progress_priority(int band) {
 // guide word g (source floats {b, g}, {r, 1}) for output i. Accumulation order per output is
 // ascending kx, as in the reference's row-major loop.
 typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Pins the accumulators at a row boundary: their row's updates happen before this
+// point and none move across it (with every row unrolled, the compiler otherwise
+// sinks all accumulation below all LUT reads and spills every weight).
+template <int P>
+__device__ __forceinline__ void fence_accumulators(f2 (&a01)[P], f2 (&a2k)[P]) {
+#pragma unroll
+    for (int i = 0; i < P; ++i) __asm__ volatile("" : "+v"(a01[i]), "+v"(a2k[i]));
+}
 
 // PK: accumulate with v_pk_fma_f32 ({s0,s1} and {s2,sk} pairs). Measured on gfx950:
 // +3 % for the adaptive kernel, -10 % for the bilateral kernel (the {r, 1} pairs
