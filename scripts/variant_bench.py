@@ -23,6 +23,11 @@ j9, j15 = _BilateralImpl(W, H, 9), _BilateralImpl(W, H, 15)
 cases += [("joint_r4", lambda s, d: j9.joint_bilateral_filter(s, guide, d)),
           ("joint_r7", lambda s, d: j15.joint_bilateral_filter(s, guide, d)),
           ("texture_k5_nitr1", _TextureImpl(W, H, 5, 1).execute)]
+if "--r15" in sys.argv:  # one 2048-row slab of the C5 frame (16384 wide, ksize 31)
+    s15 = [torch.randint(0, 255, (2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    d15 = torch.empty((2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda")
+    b31 = _BilateralImpl(16384, 2048 + 30, 31)
+    cases += [("bilateral_r15_slab", lambda s, d: b31.bilateral_filter(s15[0], d15))]
 for name, f in cases:
     for i in range(3): f(srcs[i % 6], dst)
     torch.cuda.synchronize()
@@ -34,6 +39,7 @@ for name, f in cases:
     res[name + "_us"] = round(e0.elapsed_time(e1) / n * 1e3, 1)
 print(json.dumps(res))
 '''
-for so in sys.argv[1:]:
-    r = subprocess.run([sys.executable, "-c", CODE, so], capture_output=True, text=True, timeout=300)
+extra = [a for a in sys.argv[1:] if a.startswith("--")]
+for so in [a for a in sys.argv[1:] if not a.startswith("--")]:
+    r = subprocess.run([sys.executable, "-c", CODE, so] + extra, capture_output=True, text=True, timeout=300)
     print(os.path.basename(so), r.stdout.strip() or r.stderr[-500:], flush=True)

@@ -31,7 +31,7 @@ __device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
 #endif
 
 #ifndef VIP_BIL_UNROLL_MAX_R
-#define VIP_BIL_UNROLL_MAX_R 8
+#define VIP_BIL_UNROLL_MAX_R 15
 #endif
 template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {

@@ -128,7 +128,8 @@ struct HwDispatch {
 // one body per distinct half-width -- half the code, but the register allocator then
 // copies every accumulator at each join (2 x 32 v_mov per row for 8 outputs, found
 // in the ISA). Measured: bilateral r=7 240 -> 226 us, joint r=4 94 -> 85 us unrolled;
-// the adaptive kernel (larger bodies) and r=15 (C5) are faster with the loop.
+// r=15 (C5, 16384 x 2048 slab) 3283 -> 3211 us; the adaptive kernel (larger bodies)
+// is no faster unrolled and keeps the loop.
 template <int R, bool UNROLL, class F>
 __device__ __forceinline__ void for_each_row(F&& f) {
     if constexpr (UNROLL) {
