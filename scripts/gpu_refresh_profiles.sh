@@ -11,8 +11,8 @@ for c in c2 c3 c4 c5; do
   rc=$?; echo "bench $c rc=$rc"; cut -c1-300 gpurun_out/bench_$c.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_$c.err; exit $rc; }
 done
 for c in c2 c3 c4 c5; do
-  steps=10; [ $c = c5 ] && steps=3
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python bench.py --config $c --steps $steps --warmup 1 --no-cpu-baseline > gpurun_out/prof_$c.log 2>&1
+  steps=20; [ $c = c5 ] && steps=5
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$c -o run --output-format csv -- python bench.py --config $c --steps $steps --warmup 3 --no-cpu-baseline > gpurun_out/prof_$c.log 2>&1
   rc=$?; echo "rocprof $c rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 for c in ${PMC_CFGS:-}; do
