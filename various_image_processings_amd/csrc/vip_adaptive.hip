@@ -16,6 +16,9 @@
 #ifndef VIP_ADA_P
 #define VIP_ADA_P 4
 #endif
+#ifndef VIP_ADA_UNROLL  // straight-line tile rows (for_each_row); measured no faster here
+#define VIP_ADA_UNROLL 0
+#endif
 
 namespace vip {
 
@@ -231,7 +234,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
         #pragma unroll
             for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
-            for_each_row<R, false>([&](const int ky, auto hwc) {
+            for_each_row<R, (VIP_ADA_UNROLL != 0)>([&](const int ky, auto hwc) {
                     constexpr int HW = decltype(hwc)::value;
                     const int aky = ky < 0 ? -ky : ky;
                     set_progress_priority((ky + R) * 4 / (2 * R + 1));
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     };
                     row_taps<HW, G::L, C0, NC, FMA, true, P, false>(plane, plane, row_off, wsv, lut_bytes, widx, a01,
                                                                     a2k);
+                    if constexpr (VIP_ADA_UNROLL != 0) fence_accumulators(a01, a2k);
             });
 
             uint32_t o[P];
