@@ -242,9 +242,10 @@ namespace vip {
 //   XR : image pixels as RGBX words, T (+) (2R+1) (origin 4-px aligned)
 //   MR : gradient magnitude, T (+) 2R
 //   H  : horizontal window aggregates of the image rows of T (+) 2R at the blur
-//        columns of T (+) R: {R|B<<16 sums, G sums, max|(1023-min)<<16 of the
-//        byte sums r+g+b} -- the separable part of the box blur and of the
-//        intensity extremes (integer sums and max/min are order-free, so exact)
+//        columns of T (+) R: {R|B<<16 sums, max|(1023-min)<<16 of the byte sums
+//        r+g+b, G sums as u16} -- the separable part of the box blur and of the
+//        intensity extremes (integer sums and max/min are order-free, so exact).
+//        2.5 words per position keep the tile at 32 KiB: 5 workgroups per CU
 //   BR, RR : blurred RGB and rtv, T (+) R (aliases XR/H once those are consumed)
 // The magnitude sum is NOT separable: it is accumulated per blur position in the
 // reference's row-major order. Bit-exact with the stage kernels: x/3.f is
@@ -277,7 +278,7 @@ struct GfGeom {
     static constexpr int XR_WORDS = XW * XH;
     static constexpr int HPL = HWP * HH;                // one H plane
     static constexpr int BPL = BW * BHP;                // one BR/RR plane
-    static constexpr int A_WORDS = cmax(XR_WORDS + 3 * HPL, 4 * BPL);
+    static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL);  // H: RB, MX words + G as u16
     static constexpr int WORDS = A_WORDS + MW * MH;
     static constexpr int NR1 = HH * (HWP / kGfH1);      // pass-1 runs
     static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
@@ -328,7 +329,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     constexpr bool PACKRB = K * K * 255 < 65536;  // R|B<<16 vertical sums stay in 16 bits
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* XR = lds;
-    uint32_t* H = lds + G::XR_WORDS;                    // 3 planes of HPL
+    uint32_t* H = lds + G::XR_WORDS;                    // RB plane, MX plane (HPL words each)
+    uint16_t* HG = reinterpret_cast<uint16_t*>(H + 2 * G::HPL);  // G sums (<= K * 255) as u16
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
     float* MR = reinterpret_cast<float*>(lds + G::A_WORDS);
@@ -414,11 +416,13 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
         win_sum<kGfH1, K>(gg, og);
         win_op<kGfH1, K>(mx, omx, pk_max_u16);
         uint32_t* h = H + hr * G::HWP + hc0;
+        static_assert(kGfH1 == 8, "one b128 store of 8 u16 G sums");
+        *reinterpret_cast<uint4*>(HG + hr * G::HWP + hc0) =
+            make_uint4(og[0] | (og[1] << 16), og[2] | (og[3] << 16), og[4] | (og[5] << 16), og[6] | (og[7] << 16));
 #pragma unroll
         for (int j = 0; j < kGfH1; j += 4) {
             *reinterpret_cast<uint4*>(h + j) = make_uint4(orb[j], orb[j + 1], orb[j + 2], orb[j + 3]);
-            *reinterpret_cast<uint4*>(h + G::HPL + j) = make_uint4(og[j], og[j + 1], og[j + 2], og[j + 3]);
-            *reinterpret_cast<uint4*>(h + 2 * G::HPL + j) = make_uint4(omx[j], omx[j + 1], omx[j + 2], omx[j + 3]);
+            *reinterpret_cast<uint4*>(h + G::HPL + j) = make_uint4(omx[j], omx[j + 1], omx[j + 2], omx[j + 3]);
         }
     }
     __syncthreads();
@@ -447,8 +451,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 #pragma unroll
             for (int t = 0; t < NV; ++t) {
                 hrb[t] = H[(p0 + t) * G::HWP + c];
-                hg[t] = H[G::HPL + (p0 + t) * G::HWP + c];
-                hmx[t] = H[2 * G::HPL + (p0 + t) * G::HWP + c];
+                hg[t] = HG[(p0 + t) * G::HWP + c];
+                hmx[t] = H[G::HPL + (p0 + t) * G::HWP + c];
             }
             if constexpr (PACKRB) {
                 win_sum<kGfV2, K>(hrb, s0);
@@ -503,8 +507,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
                         a0 += rbv & 0xffffu;
                         a2 += rbv >> 16;
                     }
-                    a1 += H[G::HPL + hi_];
-                    am = pk_max_u16(am, H[2 * G::HPL + hi_]);
+                    a1 += HG[hi_];
+                    am = pk_max_u16(am, H[G::HPL + hi_]);
                     const float* mrow = MR + (hrow + ky) * G::MW + hcol;
 #pragma unroll
                     for (int kx = 0; kx < K; ++kx) {
