@@ -137,16 +137,18 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
 #ifndef VIP_JBF_MAXW
 #define VIP_JBF_MAXW 16
 #endif
-// Outputs per thread: 8 for the plain filter; the joint filter's second plane and
-// prefetch registers push P = 8 past 128 VGPRs (spills), so it takes 4 by default.
-#ifndef VIP_JBF_P
-#define VIP_JBF_P 4
+// Outputs per thread: 8 for the plain filter. The joint filter's second plane and
+// prefetch registers push 8 outputs past 128 VGPRs as the radius grows (spilled
+// VGPRs: 0 up to R = 3, 1 at R = 4, 14 at R = 7, 36 at R = 8, 69+ beyond); 8 outputs
+// still win up to R = 7 (measured: r=4 84 -> 79 us, r=7 214 -> 206 us), 4 above.
+#ifndef VIP_JBF_P8_MAX_R
+#define VIP_JBF_P8_MAX_R 7
 #endif
 #ifndef VIP_BIL_P
 #define VIP_BIL_P 8
 #endif
 template <int R, int PLANES>
-constexpr int outputs_per_thread() { return PLANES == 2 ? VIP_JBF_P : VIP_BIL_P; }
+constexpr int outputs_per_thread() { return PLANES == 2 ? (R <= VIP_JBF_P8_MAX_R ? 8 : 4) : VIP_BIL_P; }
 template <int R, int PLANES>
 constexpr int lut_copies() {
     constexpr int P = outputs_per_thread<R, PLANES>();
