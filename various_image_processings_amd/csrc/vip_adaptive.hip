@@ -285,12 +285,8 @@ static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
                         (adaptive_vbox<R, P, WAVES>() ? 4 * TH * G::GROUPS * 4 : 0);
     static_assert(LDS <= kLdsBudget, "adaptive tile does not fit LDS");
     auto kern = adaptive_kernel<R, WAVES, FMA, P>;
-    static bool attr_done = false;
-    if (!attr_done) {
-        VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
-        attr_done = true;
-    }
+    static std::atomic<unsigned long long> attr_devs{0};
+    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
     args.tiles_x = (a.width + G::TW - 1) / G::TW;
     args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);

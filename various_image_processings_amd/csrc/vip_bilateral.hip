@@ -168,12 +168,8 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     constexpr int TH = WAVES * 4;
     constexpr int LDS = lds_bytes<R, WAVES, PLANES, 768 * COPIES, P>();
     auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P>;
-    static bool attr_done = false;  // benign race: idempotent attribute set
-    if (!attr_done) {
-        VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
-        attr_done = true;
-    }
+    static std::atomic<unsigned long long> attr_devs{0};
+    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
     args.tiles_x = (a.width + Geom<R, P>::TW - 1) / Geom<R, P>::TW;
     args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 
@@ -45,3 +46,19 @@ __host__ __device__ constexpr int circle_hw(int R, int ky) { return isqrt_floor(
         hipError_t _e = (expr);                              \
         if (_e != hipSuccess) return (int)_e;                \
     } while (0)
+
+namespace vip {
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per kernel and device (the
+// attribute is per device and one process may drive several). `devs` is the
+// caller's per-kernel static bitmask; concurrent first calls set it twice, which
+// is harmless.
+inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned long long>& devs) {
+    int dev = 0;
+    VIP_HIP_CHECK(hipGetDevice(&dev));
+    const unsigned long long bit = 1ull << (dev & 63);
+    if (devs.load(std::memory_order_relaxed) & bit) return 0;
+    VIP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    devs.fetch_or(bit, std::memory_order_relaxed);
+    return 0;
+}
+}  // namespace vip

@@ -42,16 +42,18 @@ struct StencilArgs {
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 
-// One workgroup per CU (the 96 KiB LUT fills most of the CU's LDS), each striding
-// over tiles; fewer blocks than CUs when the frame has fewer tiles.
+// One workgroup per CU of the current device (the 96 KiB LUT fills most of the CU's
+// LDS), each striding over tiles; fewer blocks than CUs when the frame has fewer tiles.
 inline int persistent_blocks(int tiles) {
-    static int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-            n = 256;
-        return n;
-    }();
+    static std::atomic<int> cus_by_dev[64];  // CU count per device, 0 = not queried yet
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    int cus = cus_by_dev[dev & 63].load(std::memory_order_relaxed);
+    if (cus == 0) {
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        cus_by_dev[dev & 63].store(cus, std::memory_order_relaxed);
+    }
     return tiles < cus ? tiles : cus;
 }
 

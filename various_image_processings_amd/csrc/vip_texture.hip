@@ -645,12 +645,8 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int 
     constexpr int LDS = 4 * GfGeom<R>::WORDS;
     static_assert(LDS <= kLdsBudget, "fused guide tile does not fit LDS");
     auto kern = texture_guide_fused_kernel<R, CPP>;
-    static bool attr_done = false;
-    if (!attr_done) {
-        VIP_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, LDS));
-        attr_done = true;
-    }
+    static std::atomic<unsigned long long> attr_devs{0};
+    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     if (gy1 <= gy0) return 0;
     dim3 grid((width + kGfTW - 1) / kGfTW, (gy1 - gy0 + kGfTH - 1) / kGfTH);
     hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
