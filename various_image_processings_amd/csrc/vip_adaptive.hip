@@ -16,8 +16,8 @@
 #ifndef VIP_ADA_P
 #define VIP_ADA_P 4
 #endif
-#ifndef VIP_ADA_UNROLL  // straight-line tile rows (for_each_row); measured no faster here
-#define VIP_ADA_UNROLL 0
+#ifndef VIP_ADA_UNROLL  // straight-line tile rows (for_each_row): 384 -> 368 us with scalar taps
+#define VIP_ADA_UNROLL 1
 #endif
 
 namespace vip {
@@ -49,6 +49,9 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     // over them. Fits the LDS for R <= 8; larger radii keep the per-thread square sums.
     constexpr int VW = G::GROUPS * 4;          // plane words in use per row (TW + 2L)
     constexpr bool VBOX = adaptive_vbox<R, P, WAVES>();
+    // straight-line rows where the separable box sums apply (R <= 8); the larger
+    // radii keep the row loop (code size and build time)
+    constexpr bool ROW_UNROLL = VIP_ADA_UNROLL != 0 && VBOX;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
     uint32_t* const plane = lds + lut_words(true);
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
         #pragma unroll
             for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
 
-            for_each_row<R, (VIP_ADA_UNROLL != 0)>([&](const int ky, auto hwc) {
+            for_each_row<R, ROW_UNROLL>([&](const int ky, auto hwc) {
                     constexpr int HW = decltype(hwc)::value;
                     const int aky = ky < 0 ? -ky : ky;
                     set_progress_priority((ky + R) * 4 / (2 * R + 1));
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     };
                     row_taps<HW, G::L, C0, NC, FMA, false, P, false>(plane, plane, row_off, wsv, lut_bytes, widx, a01,
                                                                      a2k);
-                    if constexpr (VIP_ADA_UNROLL != 0) fence_accumulators(a01, a2k);
+                    if constexpr (ROW_UNROLL) fence_accumulators(a01, a2k);
             });
 
             uint32_t o[P];

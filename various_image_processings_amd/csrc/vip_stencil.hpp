@@ -130,8 +130,7 @@ struct HwDispatch {
 // one body per distinct half-width -- half the code, but the register allocator then
 // copies every accumulator at each join (2 x 32 v_mov per row for 8 outputs, found
 // in the ISA). Measured: bilateral r=7 240 -> 226 us, joint r=4 94 -> 85 us unrolled;
-// r=15 (C5, 16384 x 2048 slab) 3283 -> 3211 us; the adaptive kernel (larger bodies)
-// is no faster unrolled and keeps the loop.
+// r=15 (C5, 16384 x 2048 slab) 3283 -> 3211 us; adaptive r=7 384 -> 368 us.
 template <int R, bool UNROLL, class F>
 __device__ __forceinline__ void for_each_row(F&& f) {
     if constexpr (UNROLL) {
@@ -330,8 +329,9 @@ __device__ __forceinline__ void fence_accumulators(f2 (&a01)[P], f2 (&a2k)[P]) {
 }
 
 // PK: accumulate with v_pk_fma_f32 ({s0,s1} and {s2,sk} pairs). Measured on gfx950:
-// +3 % for the adaptive kernel, -10 % for the bilateral kernel (the {r, 1} pairs
-// push it past 128 VGPRs), so it is a per-kernel choice.
+// slower for every kernel (bilateral -10 %; adaptive 381 us scalar vs 446 us packed,
+// together with packed offset subtracts) -- VOP3P ops do not pair with the other
+// VALU work -- so both kernels use PK = false; kept as a knob.
 // TWO: separate guide and source planes (joint bilateral); otherwise one plane.
 #ifndef VIP_ROW_LOOKAHEAD
 #define VIP_ROW_LOOKAHEAD 4  // columns between a chunk's LDS read and its first use
