@@ -270,6 +270,7 @@ def main():
                     traffic_algorithmic=6.0 * px_per_rank,
                     kernel=f"{cfg['kind']}_kernel<R={r}>", avg_launch_ms=round(kernel_ms, 4),
                     flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
+                    gtaps_per_s=round(taps * px_per_rank / (kernel_ms * 1e-3) / 1e9, 1),
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
                              bytes_per_px=6))
 
