@@ -245,7 +245,8 @@ namespace vip {
 //        columns of T (+) R: {R|B<<16 sums, max|(1023-min)<<16 of the byte sums
 //        r+g+b, G sums as u16} -- the separable part of the box blur and of the
 //        intensity extremes (integer sums and max/min are order-free, so exact).
-//        2.5 words per position keep the tile at 32 KiB: 5 workgroups per CU
+//        2.5 words per position, and MR stored over XR, keep the tile at 26 KiB:
+//        6 workgroups per CU
 //   BR, RR : blurred RGB and rtv, T (+) R (aliases XR/H once those are consumed)
 // The magnitude sum is NOT separable: it is accumulated per blur position in the
 // reference's row-major order. Bit-exact with the stage kernels: x/3.f is
@@ -278,8 +279,11 @@ struct GfGeom {
     static constexpr int XR_WORDS = XW * XH;
     static constexpr int HPL = HWP * HH;                // one H plane
     static constexpr int BPL = BW * BHP;                // one BR/RR plane
-    static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL);  // H: RB, MX words + G as u16
-    static constexpr int WORDS = A_WORDS + MW * MH;
+    // XR, then MR in its place (gradients wait in registers until XR is consumed);
+    // H after it (RB, MX words + G as u16); BR/RR and the guide tile GT reuse it all
+    static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL + kGfTW * kGfTH);
+    static constexpr int WORDS = A_WORDS;
+    static_assert(MW * MH <= XR_WORDS, "MR reuses the XR region");
     static constexpr int NR1 = HH * (HWP / kGfH1);      // pass-1 runs
     static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
     static constexpr int IT2 = (NR2 + kGfNT - 1) / kGfNT;
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     uint16_t* HG = reinterpret_cast<uint16_t*>(H + 2 * G::HPL);  // G sums (<= K * 255) as u16
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
-    float* MR = reinterpret_cast<float*>(lds + G::A_WORDS);
+    float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
     const int x0 = blockIdx.x * kGfTW, y0 = gy0 + blockIdx.y * kGfTH;
     const int tid = threadIdx.x;
     // region origins (image coordinates)
@@ -382,7 +386,12 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //     read directly (XR[c +- e] == X(clamp(c +- e))). sum_c h^2 + v^2 is an exact
     //     integer (< 2^24), equal to the reference's float sums: v_dot2 on the
     //     {c0, c2} 16-bit difference pairs, a mad for c1.
-    for (int i = tid; i < G::MW * G::MH; i += kGfNT) {
+    constexpr int NM = G::MW * G::MH, KM = (NM + kGfNT - 1) / kGfNT;
+    float mrv[KM];  // this thread's gradients, stored to MR (over XR) after pass 1
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        const int i = tid + k * kGfNT;
+        if (NM % kGfNT != 0 && i >= NM) continue;
         const int qy = i / G::MW, qx = i - qy * G::MW;
         const int cx = clampi(mr0x + qx, 0, W1) - xr0, cy = clampi(mr0y + qy, H0, H1) - yr0;
         const uint32_t* c = XR + cy * G::XW + cx;
@@ -393,7 +402,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
         const int v1 = (int)__builtin_amdgcn_ubfe(D, 8, 8) - (int)__builtin_amdgcn_ubfe(U, 8, 8);
         const int ss = __builtin_amdgcn_sdot2(h02, h02, __builtin_amdgcn_sdot2(v02, v02, h1 * h1 + v1 * v1, false),
                                               false);
-        MR[i] = __builtin_sqrtf((float)ss);
+        mrv[k] = __builtin_sqrtf((float)ss);
     }
     // 2b. pass 1: H = horizontal K-window aggregates, kGfH1 adjacent columns per thread.
     //     H row h <-> image row y0 - 2R + h (XR row h + 1); H column c <-> image column
@@ -424,6 +433,13 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
             *reinterpret_cast<uint4*>(h + j) = make_uint4(orb[j], orb[j + 1], orb[j + 2], orb[j + 3]);
             *reinterpret_cast<uint4*>(h + G::HPL + j) = make_uint4(omx[j], omx[j + 1], omx[j + 2], omx[j + 3]);
         }
+    }
+    __syncthreads();  // XR is consumed (gradients and pass 1): MR takes its place
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+        const int i = tid + k * kGfNT;
+        if (NM % kGfNT != 0 && i >= NM) continue;
+        MR[i] = mrv[k];
     }
     __syncthreads();
 
@@ -560,8 +576,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //    found once and shared; scanning those rows in order with strict > then
     //    gives the row-major first argmin. Alpha blend per output.
     const float sigma_alpha = 1.f / (float)(5 * ksize);
-    uint32_t* GT = reinterpret_cast<uint32_t*>(MR);  // guide tile as RGBX words (MR is consumed)
-    static_assert(kGfTW * kGfTH <= G::MW * G::MH, "guide tile does not fit the MR region");
+    uint32_t* GT = lds + 4 * G::BPL;  // guide tile as RGBX words, after BR/RR
     for (int run = tid; run < (kGfTH / kGfRun) * kGfTW; run += kGfNT) {
         const int tx = run % kGfTW, ty0 = (run / kGfTW) * kGfRun;
         const int x = x0 + tx;
