@@ -1,0 +1,68 @@
+// Exactness check of the bilateral epilogue's division (vip_stencil.hpp div_by_sumk):
+//   y  = rcp(k) refined by one Newton step          -- must equal RN(1/k)
+//   q0 = RN(s * y); r = fma(-k, q0, s); q = fma(r, y, q0)  -- must equal RN(s / k)
+// (a) the reciprocal EXHAUSTIVELY for every float k in [1, 1024) -- the sum of
+//     weights of a bilateral/joint window: the centre tap weighs exactly 1, every
+//     tap at most 1, at most 31*31 taps;
+// (b) the quotient for 2^30 pseudo-random (s, k), s in [0, 255 k], and for s at the
+//     float midpoints' neighbourhoods -- Markstein's theorem makes (b) follow from (a),
+//     this is the empirical cross-check.
+// Exit status 0 iff no mismatch against the IEEE divide (hipcc default, correctly
+// rounded). Run on the GPU: tests/test_gpu_parity.py::test_epilogue_division_exact.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "vip_stencil.hpp"
+
+__device__ unsigned long long g_bad[2];
+
+__global__ void recip_all(uint32_t lo_bits, uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float k = __uint_as_float(lo_bits + i);
+    const float y = vip::recip_exact(k);
+    const float want = 1.0f / k;  // IEEE, correctly rounded
+    if (__float_as_uint(y) != __float_as_uint(want)) atomicAdd(&g_bad[0], 1ull);
+}
+
+__device__ __forceinline__ uint32_t mix(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return (uint32_t)x;
+}
+
+__global__ void quot_random(uint64_t base) {
+    const uint64_t i = base + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint32_t a = mix(2 * i), b = mix(2 * i + 1);
+    const float k = 1.0f + (float)(a >> 9) * (1023.0f / 8388608.0f);  // [1, 1024)
+    float s;
+    if (b & 1) {
+        s = (float)(b >> 8) * (255.0f / 16777216.0f) * k;  // uniform in [0, 255 k)
+    } else {
+        // near a float midpoint of the quotient: s = k * (m + half ulp) +- a few ulp
+        const float m = (float)(b >> 9) * (255.0f / 8388608.0f);
+        const float mid = m + 0.5f * (__uint_as_float(__float_as_uint(m) + 1) - m);
+        s = __uint_as_float(__float_as_uint(mid * k) + (int)(b >> 28) - 8);
+    }
+    const float y = vip::recip_exact(k);
+    const float q = vip::div_by_sumk(s, k, y);
+    const float want = s / k;
+    if (__float_as_uint(q) != __float_as_uint(want)) atomicAdd(&g_bad[1], 1ull);
+}
+
+int main() {
+    unsigned long long zero[2] = {0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero)) != hipSuccess) return 2;
+    const uint32_t lo = 0x3f800000u, hi = 0x44800000u;  // bit patterns of 1.0f and 1024.0f
+    const uint32_t n = hi - lo;
+    hipLaunchKernelGGL(recip_all, dim3((n + 255) / 256), dim3(256), 0, 0, lo, n);
+    const uint64_t per = 1ull << 26;
+    for (int rep = 0; rep < 16; ++rep)
+        hipLaunchKernelGGL(quot_random, dim3((unsigned)(per / 256)), dim3(256), 0, 0, rep * per);
+    unsigned long long bad[2];
+    if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
+    std::printf("reciprocal: %u floats k in [1, 1024), %llu mismatches\n", n, bad[0]);
+    std::printf("quotient: %llu random (s, k), %llu mismatches\n", (unsigned long long)(16 * per), bad[1]);
+    return (bad[0] || bad[1]) ? 1 : 0;
+}

@@ -327,3 +327,26 @@ def test_texture_iterate_rows_band(dev, oracle):
     want = oracle.texture(frame, k, 1)
     got = dev.get(band)
     assert np.array_equal(got, want[40:71]), _mismatch(got, want[40:71])
+
+
+def test_epilogue_division_exact():
+    """The bilateral/joint epilogue divides by sumk via one reciprocal (vip_stencil.hpp
+    recip_exact/div_by_sumk). microbench/div_check checks RN(1/k) for EVERY float k in
+    [1, 1024) and 2^30 quotients against the IEEE divide on the GPU."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "..", "microbench", "div_check")
+    assert os.path.exists(exe), "build first: make -C various_image_processings_amd/csrc"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
+
+
+@pytest.mark.parametrize("k,ss,sc", [(31, 1000.0, 1000.0), (5, 0.1, 0.1), (15, 3.0, 1e4), (7, 1e4, 0.5)])
+def test_bilateral_extreme_sigmas(dev, oracle, k, ss, sc):
+    """sumk at both ends of [1, 961]: flat weights (every tap ~1) and a lone centre tap."""
+    img = oracle.random_image(96, 80)
+    for guide in (None, np.ascontiguousarray(img[::-1, ::-1])):
+        got = _bilateral_gpu(dev, img, k, ss, sc, guide=guide)
+        want = oracle.bilateral(img, k, ss, sc) if guide is None else oracle.joint_bilateral(img, guide, k, ss, sc)
+        assert np.array_equal(got, want), _mismatch(got, want)

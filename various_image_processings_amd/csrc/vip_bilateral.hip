@@ -33,6 +33,9 @@ __device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
 #ifndef VIP_BIL_UNROLL_MAX_R
 #define VIP_BIL_UNROLL_MAX_R 15
 #endif
+#ifndef VIP_BIL_RCP  // epilogue: one exact reciprocal per output instead of 3 IEEE divides
+#define VIP_BIL_RCP 1
+#endif
 template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
@@ -114,7 +117,7 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
             });
 
             uint32_t o[P];
-            finish_outputs(a01, a2k, o);
+            finish_outputs<P, VIP_BIL_RCP != 0>(a01, a2k, o);
             store_px(a, ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);

@@ -404,13 +404,38 @@ __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t*
     }
 }
 
-// dst = u8(sum_c / sumk + 0.5f) for the P outputs, packed as RGBX words
-template <int P>
+// RN(1/k) for k in [1, 1024): hardware rcp (1 ulp) + one Newton step. Verified
+// exhaustively over every float of that range by microbench/div_check.hip.
+__device__ __forceinline__ float recip_exact(float k) {
+    const float y0 = __builtin_amdgcn_rcpf(k);
+    return __builtin_fmaf(__builtin_fmaf(-k, y0, 1.0f), y0, y0);
+}
+
+// RN(s / k) given y = RN(1/k) (Markstein): q0 = RN(s y) is within 1 ulp of s/k, the
+// residual s - k q0 is exact under fma, and one correction rounds correctly. Needs
+// no over/underflow: s in [0, 255 k], k in [1, 1024). Cross-checked on 2^30 random
+// and near-midpoint quotients by microbench/div_check.hip.
+__device__ __forceinline__ float div_by_sumk(float s, float k, float y) {
+    const float q0 = s * y;
+    return __builtin_fmaf(__builtin_fmaf(-k, q0, s), y, q0);
+}
+
+// dst = u8(sum_c / sumk + 0.5f) for the P outputs, packed as RGBX words. RCP: the
+// window holds its centre tap with weight exactly 1 (bilateral, joint), so sumk is in
+// [1, 1024) and the three divides share one exact reciprocal; the adaptive filter's
+// sumk may be tiny or 0 and keeps the IEEE divide.
+template <int P, bool RCP = false>
 __device__ __forceinline__ void finish_outputs(const f2 (&a01)[P], const f2 (&a2k)[P], uint32_t (&o)[P]) {
 #pragma unroll
     for (int i = 0; i < P; ++i) {
         const float sk = a2k[i].y;
-        o[i] = f2u8(a01[i].x / sk + 0.5f) | (f2u8(a01[i].y / sk + 0.5f) << 8) | (f2u8(a2k[i].x / sk + 0.5f) << 16);
+        if constexpr (RCP) {
+            const float y = recip_exact(sk);
+            o[i] = f2u8(div_by_sumk(a01[i].x, sk, y) + 0.5f) | (f2u8(div_by_sumk(a01[i].y, sk, y) + 0.5f) << 8) |
+                   (f2u8(div_by_sumk(a2k[i].x, sk, y) + 0.5f) << 16);
+        } else {
+            o[i] = f2u8(a01[i].x / sk + 0.5f) | (f2u8(a01[i].y / sk + 0.5f) << 8) | (f2u8(a2k[i].x / sk + 0.5f) << 16);
+        }
     }
 }
 
