@@ -40,6 +40,8 @@ sys.path.insert(0, ROOT)
 
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (== f32 MFMA) peak
+VALU_SIMDS = 1024            # 256 CUs x 4 SIMDs
+VALU_CYCLES_PER_INSTR = 2    # a wave64 VALU instruction issues over 2 cycles (MI355X_MICROARCH.md)
 NBUF = 12
 BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
 
@@ -121,6 +123,33 @@ def pmc_traffic(config: str, kernels: list, per_step: int = 1):
             return None, None
         total += hit[0]["traffic_bytes"]
     return total * per_step, os.path.relpath(files[-1], ROOT)
+
+
+def valu_issue(config: str, kernel: str, launch_ms: float):
+    """VALU-issue roofline of one kernel: its SQ_INSTS_VALU wave-instructions per launch
+    (committed PMC summary) / the live event-timed launch, against 1024 SIMDs issuing one
+    wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md) at the 2.4 GHz maximum
+    clock and at the clock the chip held under this load (GRBM_GUI_ACTIVE / 8 XCDs /
+    launch time). None when no summary matches."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        ks = json.load(fh)["kernels"]
+    hit = [v["counters"] for n, v in ks.items() if n.startswith(kernel) and "SQ_INSTS_VALU" in v.get("counters", {})]
+    if not hit:
+        return None
+    c = hit[0]
+    achieved = c["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9
+    peak = VALU_SIMDS * 2.4 / VALU_CYCLES_PER_INSTR
+    out = dict(achieved=round(achieved, 1), peak=round(peak, 1), unit="G wave-instr/s",
+               frac=round(achieved / peak, 4), wave_instr_per_launch=c["SQ_INSTS_VALU"],
+               source=os.path.relpath(files[-1], ROOT))
+    if c.get("GRBM_GUI_ACTIVE"):
+        clk = c["GRBM_GUI_ACTIVE"] / 8 / (launch_ms * 1e-3) / 1e9
+        out.update(load_clock_ghz=round(clk, 2), frac_at_load_clock=round(achieved / (VALU_SIMDS * clk / VALU_CYCLES_PER_INSTR), 4))
+    return out
 
 
 def main():
@@ -273,6 +302,8 @@ def main():
                     gtaps_per_s=round(taps * px_per_rank / (kernel_ms * 1e-3) / 1e9, 1),
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
                              bytes_per_px=6))
+        if world == 1:  # the committed PMC summaries are whole-frame launches
+            roof["valu_issue"] = valu_issue(args.config, f"void vip::{cfg['kind']}_kernel<{r},", kernel_ms)
 
     out = {
         "metric": BASELINE_METRIC if args.config == "c2" else f"Mpixels/sec {cfg['workload']}",
