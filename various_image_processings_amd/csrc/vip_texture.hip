@@ -256,7 +256,14 @@ namespace vip {
 // tests/test_oracle.py::test_constant_division_is_exact), rtv divide in double
 // (CUDA profile).
 // ---------------------------------------------------------------------------
-constexpr int kGfTW = 64, kGfTH = 16, kGfNT = 256;
+#ifndef VIP_GF_TW
+#define VIP_GF_TW 64
+#endif
+#ifndef VIP_GF_TH
+#define VIP_GF_TH 16
+#endif
+constexpr int kGfTW = VIP_GF_TW, kGfTH = VIP_GF_TH, kGfNT = 256;
+static_assert(kGfTW % 4 == 0 && kGfTH % 4 == 0, "guide tile: 4-pixel groups, 4-row runs");
 constexpr int kGfH1 = 8;   // pass 1: horizontally adjacent window aggregates per thread
 constexpr int kGfV2 = 4;   // pass 2: vertically adjacent blur positions per thread
 constexpr int kGfRun = 4;  // guide: vertically adjacent outputs per thread
