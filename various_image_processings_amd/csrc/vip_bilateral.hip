@@ -26,8 +26,18 @@ __device__ __forceinline__ void vip_stamp(int blk, int wave, int t, int k) {
         vip_stamps[((blk * 16 + wave) * 8 + t) * 3 + k] = __builtin_amdgcn_s_memtime();
 }
 #define VIP_STAMP(t, k) vip_stamp(blockIdx.x, wave, t, k)
+// [block][entry shader clock, entry 100 MHz real time, exit clock, exit real time]
+__device__ unsigned long long vip_rt[256 * 4];
+__device__ __forceinline__ void vip_rt_stamp(int k) {
+    if (threadIdx.x == 0 && blockIdx.x < 256) {
+        vip_rt[blockIdx.x * 4 + 2 * k] = __builtin_amdgcn_s_memtime();
+        vip_rt[blockIdx.x * 4 + 2 * k + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+#define VIP_RT_STAMP(k) vip_rt_stamp(k)
 #else
 #define VIP_STAMP(t, k)
+#define VIP_RT_STAMP(k)
 #endif
 
 #ifndef VIP_BIL_UNROLL_MAX_R
@@ -57,6 +67,7 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     const uint32_t lane4 = (uint32_t)(lane & (COPIES - 1)) << 2;  // this lane's LUT copy
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
+    VIP_RT_STAMP(0);
     // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
     int tile = blockIdx.x;
     TilePrefetch<R, ROWS, NT, P> pg, ps;
@@ -121,7 +132,10 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
             store_px(a, ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);
-        if (next >= a.tiles_total) break;
+        if (next >= a.tiles_total) {
+            VIP_RT_STAMP(1);
+            break;
+        }
         __syncthreads();  // every wave is done reading this tile
         pg.commit(gplane);
         if constexpr (JOINT) ps.commit(splane);
@@ -215,6 +229,9 @@ int launch_bilateral_plain_fma(int radius, const StencilArgs& a, hipStream_t s) 
 }  // namespace vip
 extern "C" int vip_debug_read_stamps(void* host, size_t bytes) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vip::vip_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+extern "C" int vip_debug_read_rt(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vip::vip_rt), bytes, 0, hipMemcpyDeviceToHost);
 }
 namespace vip {
 #endif
