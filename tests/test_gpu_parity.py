@@ -280,6 +280,49 @@ def test_host_frame_async_path(dev, oracle):
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
+def test_split_stream_host_pipeline(dev, oracle):
+    """Upload, filter and download on three streams ordered by vip_event_* (the split
+    host-frame pipeline of samples/vip_host_pipeline.cpp): same bytes as the oracle."""
+    import ctypes
+    from various_image_processings_amd._lib import call
+    img = oracle.random_image(257, 99)
+    n = img.nbytes
+    h_in, h_out = ctypes.c_void_p(), ctypes.c_void_p()
+    st = [ctypes.c_void_p() for _ in range(3)]
+    ev = [ctypes.c_void_p() for _ in range(3)]
+    call("vip_host_alloc", ctypes.byref(h_in), n)
+    call("vip_host_alloc", ctypes.byref(h_out), n)
+    for x in st:
+        call("vip_stream_create", ctypes.byref(x))
+    for x in ev:
+        call("vip_event_create", ctypes.byref(x))
+    try:
+        ctypes.memmove(h_in.value, img.ctypes.data, n)
+        ctypes.memset(h_out.value, 0, n)
+        d_src, d_dst = dev.empty(img.shape), dev.empty(img.shape)
+        f = _BilateralImpl(257, 99, 15)
+        su, sc, sd = st
+        call("vip_upload_async", ctypes.c_void_p(d_src.data_ptr()), h_in, n, su)
+        call("vip_event_record", ev[0], su)
+        call("vip_stream_wait_event", sc, ev[0])
+        f.bilateral_filter(d_src, d_dst, stream=sc.value)
+        call("vip_event_record", ev[1], sc)
+        call("vip_stream_wait_event", sd, ev[1])
+        call("vip_download_async", h_out, ctypes.c_void_p(d_dst.data_ptr()), n, sd)
+        call("vip_event_record", ev[2], sd)
+        call("vip_event_synchronize", ev[2])
+        got = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(h_out.value)).reshape(img.shape).copy()
+    finally:
+        for x in ev:
+            call("vip_event_destroy", x)
+        for x in st:
+            call("vip_stream_destroy", x)
+        call("vip_host_free", h_in)
+        call("vip_host_free", h_out)
+    want = oracle.bilateral(img, 15)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
 def _fill_slab(dev, frame, geo):
     """The slab a rank holds after exchange_halo: own rows plus neighbour halo rows."""
     import torch

@@ -42,6 +42,11 @@ SIGNATURES = {
     "vip_download_async": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "vip_stream_create": (_c_int, [ctypes.POINTER(_c_void_p)]),
     "vip_stream_destroy": (_c_int, [_c_void_p]),
+    "vip_event_create": (_c_int, [ctypes.POINTER(_c_void_p)]),
+    "vip_event_destroy": (_c_int, [_c_void_p]),
+    "vip_event_record": (_c_int, [_c_void_p, _c_void_p]),
+    "vip_stream_wait_event": (_c_int, [_c_void_p, _c_void_p]),
+    "vip_event_synchronize": (_c_int, [_c_void_p]),
     "vip_bilateral_create": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_int, _c_float, _c_float, _c_int]),
     "vip_bilateral_destroy": (_c_int, [_c_void_p]),
     "vip_bilateral_run": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p, _c_size_t, _c_void_p]),

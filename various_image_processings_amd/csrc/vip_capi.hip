@@ -167,6 +167,16 @@ int vip_stream_create(void** stream) {
     return (int)hipStreamCreateWithFlags(reinterpret_cast<hipStream_t*>(stream), hipStreamNonBlocking);
 }
 int vip_stream_destroy(void* stream) { return (int)hipStreamDestroy((hipStream_t)stream); }
+int vip_event_create(void** event) {
+    if (!event) return VIP_ERR_INVALID_ARGUMENT;
+    return (int)hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(event), hipEventDisableTiming);
+}
+int vip_event_destroy(void* event) { return (int)hipEventDestroy((hipEvent_t)event); }
+int vip_event_record(void* event, void* stream) { return (int)hipEventRecord((hipEvent_t)event, (hipStream_t)stream); }
+int vip_stream_wait_event(void* stream, void* event) {
+    return (int)hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0);
+}
+int vip_event_synchronize(void* event) { return (int)hipEventSynchronize((hipEvent_t)event); }
 
 // ---------------------------------------------------------------- bilateral
 int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
