@@ -75,7 +75,29 @@ def parse():
     # rehearsal only: gloo + every rank on cuda:0 runs the N>1 code path on a 1-GPU box
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     p.add_argument("--same-device", action="store_true")
+    # SURVEY 8(d) inputs: (i) uniform 0..254 like test/random_array.hpp (default), (ii) narrow
+    # uniform [100, 120) like sample/benchmark/main.cpp:213, (iii) lenna tiled to the frame
+    p.add_argument("--data", default="uniform", choices=["uniform", "narrow", "lenna"])
     return p.parse_args()
+
+
+DATA_DESC = {
+    "uniform": "synthetic uniform u8 RGB (torch.randint 0..254)",
+    "narrow": "synthetic narrow uniform u8 RGB (torch.randint 100..119, sample/benchmark/main.cpp:213)",
+    "lenna": "lenna 512x512 BGR (tests/golden/lenna_bgr.npz) tiled to the frame, row offset per buffer",
+}
+
+
+def make_frames(torch, kind, rows, w, dev, gen, n):
+    """n distinct (rows, w, 3) u8 frames resident on dev."""
+    if kind == "lenna":
+        tile = torch.from_numpy(np.load(os.path.join(ROOT, "tests", "golden", "lenna_bgr.npz"))["bgr"]).to(dev)
+        reps = ((rows + 2 * 512 - 1) // 512, (w + 511) // 512, 1)
+        big = tile.repeat(*reps)
+        # a different vertical phase per buffer so the rotating frames differ
+        return [big[(37 * i) % 512:(37 * i) % 512 + rows, :w].contiguous() for i in range(n)]
+    lo, hi = (100, 120) if kind == "narrow" else (0, 255)
+    return [torch.randint(lo, hi, (rows, w, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(n)]
 
 
 def cpu_baseline(cfg) -> dict:
@@ -191,7 +213,7 @@ def main():
         frame_h = rows
         geo = None
         tex = _TextureImpl(w, rows, k, cfg["nitr"])
-        srcs = [torch.randint(0, 255, (rows, w, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(NBUF)]
+        srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
         def step(i):
@@ -204,8 +226,7 @@ def main():
         st = ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world)
         geo = st.geo
         rows = geo.own
-        srcs = [torch.randint(0, 255, (geo.slab_rows, w, 3), dtype=torch.uint8, device=dev, generator=gen)
-                for _ in range(NBUF)]
+        srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
         def step(i):
@@ -216,8 +237,7 @@ def main():
         sb = ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
         geo = sb.geo
         rows = geo.own
-        srcs = [torch.randint(0, 255, (geo.slab_rows, w, 3), dtype=torch.uint8, device=dev, generator=gen)
-                for _ in range(NBUF)]
+        srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time.
         # N>1: the halo exchange sits between kernels, so every KSAMPLE-th kernel is
@@ -317,7 +337,7 @@ def main():
         "scaling": "strong" if "frame_height" in cfg else "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic uniform u8 RGB (torch.randint 0..254), resident in HBM; f32 weights/sums",
+        "data": DATA_DESC[args.data] + ", resident in HBM; f32 weights/sums",
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows,
                    "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
