@@ -51,6 +51,10 @@ def circle_taps(r: int) -> int:
 
 
 CONFIGS = {
+    # C1 is the include/cpp (CPU) plumbing case: cpu_baseline times it; the GPU line is
+    # the same filter on the same image through the HIP path
+    "c1": dict(kind="bilateral", width=512, frame_height=512, ksize=11, data="lenna", cpu_input="lenna",
+               workload="bilateral r=5 sigma_s=10 sigma_r=30 lenna 512x512"),
     "c2": dict(kind="bilateral", width=3840, rows_per_rank=2160, ksize=15, workload="bilateral r=7 3840x2160 RGB8"),
     "c3": dict(kind="adaptive", width=3840, rows_per_rank=2160, ksize=15,
                workload="adaptive bilateral r=7 3840x2160 RGB8"),
@@ -59,10 +63,11 @@ CONFIGS = {
     "c5": dict(kind="bilateral", width=16384, frame_height=16384, ksize=31,
                workload="bilateral r=15 16384x16384 RGB8 row-tiled"),
 }
-# algorithmic FP32 operations per in-support tap (DESIGN.md): bilateral
-# ws*wc (1) + 3 fma (6) + sumk add (1) = 8; adaptive adds the offset distance
-# ((n-c)-o: 6, |.|+|.|+|.|: 2) = 16.
-FLOP_PER_TAP = {"bilateral": 8, "adaptive": 16}
+# algorithmic FP32 operations per in-support tap (SURVEY 8(d), DESIGN.md): bilateral
+# ws*wc (1) + 3 fma (6) + sumk add (1) = 8; adaptive adds the float offset distance:
+# 3 subtractions of the offset and the 2 adds of |.|+|.|+|.| = 13 (the integer
+# (n - c) differences count no FLOP).
+FLOP_PER_TAP = {"bilateral": 8, "adaptive": 13}
 
 
 def parse():
@@ -100,31 +105,67 @@ def make_frames(torch, kind, rows, w, dev, gen, n):
     return [torch.randint(lo, hi, (rows, w, 3), dtype=torch.uint8, device=dev, generator=gen) for _ in range(n)]
 
 
+def host_cores() -> tuple[int, str]:
+    """Host cores this process may use (affinity set, capped by a cgroup CPU quota
+    when one is set) and the CPU model name."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = max(1, min(n, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, model
+
+
 def cpu_baseline(cfg) -> dict:
-    """include/cpp numerics (oracle CPP profile, row-parallel threads) on a
-    bounded sample of the same workload. Test infrastructure, not the product."""
+    """include/cpp numerics (oracle CPP profile) on the host cores, row bands in
+    parallel threads, on a bounded sample of the same workload: one discarded warm-up,
+    then the mean of 10 runs (sample/benchmark/main.cpp:20-33, config.toml
+    execute_times = 10). Test infrastructure, reported beside the GPU number."""
     from oracle import oracle as o
-    threads = max(1, min(16, os.cpu_count() or 1))
-    w = cfg["width"]
-    k = cfg["ksize"]
-    if cfg["kind"] == "texture":
-        rows = 256
+    threads, model = host_cores()
+    w, k = cfg["width"], cfg["ksize"]
+    runs = 10
+    if cfg.get("cpu_input") == "lenna":
+        img = np.load(os.path.join(ROOT, "tests", "golden", "lenna_bgr.npz"))["bgr"]
+        rows = img.shape[0]
+        desc = f"lenna 512x512 (C1), bilateral ksize={k}"
+        fn = lambda: o.bilateral(img, k, profile=o.CPP, threads=threads)  # noqa: E731
+    elif cfg["kind"] == "texture":
+        # every pixel costs the same (no data-dependent work), so independent row bands
+        # (each filtered as its own frame) time the same work per pixel
+        rows = 4 * threads
         img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
+        parts = np.array_split(np.arange(rows), threads)
+        desc = f"{w}x{rows} band split in {threads} row bands, texture ksize={k} nitr={cfg['nitr']}"
+        fn = lambda: o.bands(lambda a, b: o.texture(img[a:b], k, cfg["nitr"], profile=o.CPP),  # noqa: E731
+                             [(int(p[0]), int(p[-1]) + 1) for p in parts], threads)
+    else:
+        rows = {7: 2160, 15: 64}.get(k // 2, 256)
+        img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
+        f = o.adaptive if cfg["kind"] == "adaptive" else o.bilateral
+        desc = f"{w}x{rows} {'frame' if rows == 2160 else 'band'}, {cfg['kind']} ksize={k}"
+        fn = lambda: f(img, k, profile=o.CPP, threads=threads)  # noqa: E731
+    fn()  # warm-up, discarded
+    ts = []
+    for _ in range(runs):
         t0 = time.perf_counter()
-        o.texture(img, k, cfg["nitr"], profile=o.CPP)
-        dt = time.perf_counter() - t0
-        return dict(value=rows * w / dt / 1e6, unit="Mpixels/s", cores=1, kind="port",
-                    sample=f"{w}x{rows} band, texture k={k} nitr={cfg['nitr']}, 1 thread (oracle CPP profile)")
-    rows = 2160 if k <= 15 else 256
-    img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
-    fn = o.adaptive if cfg["kind"] == "adaptive" else o.bilateral
-    fn(img[:64], k, profile=o.CPP, threads=threads)  # warm-up
-    t0 = time.perf_counter()
-    fn(img, k, profile=o.CPP, threads=threads)
-    dt = time.perf_counter() - t0
-    return dict(value=rows * w / dt / 1e6, unit="Mpixels/s", cores=threads, kind="port",
-                sample=f"{w}x{rows} frame, {cfg['kind']} ksize={k}, {threads} threads "
-                       f"(oracle CPP profile = include/cpp numerics, all k*k taps like the reference loop)")
+        fn()
+        ts.append(time.perf_counter() - t0)
+    dt = sum(ts) / runs
+    return dict(value=round(rows * w / dt / 1e6, 4), unit="Mpixels/s", cores=threads, cpu_model=model, runs=runs,
+                warmup=1, ms_per_run=round(dt * 1e3, 2), kind="port",
+                sample=f"{desc}, {threads} threads, mean of {runs} runs after 1 warm-up (oracle CPP profile = "
+                       f"include/cpp numerics, all k*k taps like the reference loop)")
 
 
 def pmc_traffic(config: str, kernels: list, per_step: int = 1):
@@ -180,6 +221,8 @@ def main():
     import torch.distributed as dist
 
     cfg = CONFIGS[args.config]
+    if "data" in cfg and args.data == "uniform":
+        args.data = cfg["data"]
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -191,15 +234,24 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-        dist.barrier()  # communicator up before the first (P2P) halo exchange
+        # a rank that cannot join (RCCL init failure, a missing peer) must end the run
+        # with a message and a non-zero status, never hang: bounded rendezvous and
+        # collective timeouts (the NCCL watchdog aborts a stuck P2P after `timeout`)
+        import datetime
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        try:
+            if args.backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=180))
+            else:
+                dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=180))
+            dist.barrier()  # communicator up before the first (P2P) halo exchange
+        except Exception as e:  # noqa: BLE001
+            print(f"bench.py rank {rank}: process group ({args.backend}) failed: {e!r}", file=sys.stderr, flush=True)
+            os._exit(3)
 
-    import various_image_processings_amd as vip
+    import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
     from various_image_processings_amd.filters import _TextureImpl
-    from various_image_processings_amd.sharded import ShardedBilateral
+    from various_image_processings_amd.sharded import ShardedBilateral, ShardedTexture, exchange_halo
 
     stream = torch.cuda.current_stream(dev)
     w = cfg["width"]
@@ -216,12 +268,11 @@ def main():
         srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
-        def step(i):
+        def run(i):
             tex.execute(srcs[i % NBUF], dsts[i % NBUF], stream=stream)
     elif cfg["kind"] == "texture":
         # row-sharded frame: one halo exchange of nitr * texture_halo_rows(k) rows per
         # frame, then shrinking ghost zones (sharded.ShardedTexture)
-        from various_image_processings_amd.sharded import ShardedTexture, exchange_halo
         frame_h = cfg["rows_per_rank"] * world
         st = ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world)
         geo = st.geo
@@ -229,8 +280,7 @@ def main():
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
-        def step(i):
-            exchange_halo(srcs[i % NBUF], geo)
+        def run(i):
             st.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
     else:
         frame_h = cfg.get("frame_height", cfg.get("rows_per_rank", 0) * world)
@@ -239,28 +289,33 @@ def main():
         rows = geo.own
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
-        # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time.
-        # N>1: the halo exchange sits between kernels, so every KSAMPLE-th kernel is
-        # bracketed by its own events (an event pair costs ~11 us of stream time,
-        # measured with rocprofv3, so not every step carries one).
-        KSAMPLE = 4
-        kstart = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        kend = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-        timed = {"on": False, "i": 0, "n": 0}
 
-        def step(i):
-            from various_image_processings_amd.sharded import exchange_halo
-            if world > 1:
-                exchange_halo(srcs[i % NBUF], geo)
-            sample = timed["on"] and world > 1 and timed["i"] % KSAMPLE == 0
-            if sample:
-                kstart[timed["n"]].record(stream)
+        def run(i):
             sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
-            if sample:
-                kend[timed["n"]].record(stream)
-                timed["n"] += 1
-            if timed["on"]:
-                timed["i"] += 1
+
+    # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time.
+    # N>1: the halo exchange sits between kernels, so every KSAMPLE-th step is
+    # bracketed by events before the exchange, between exchange and kernel(s), and
+    # after them (an event pair costs ~11 us of stream time, measured with rocprofv3,
+    # so not every step carries them): exchange_ms and kernel_ms per rank.
+    KSAMPLE = 4
+    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    timed = {"on": False, "i": 0, "n": 0}
+
+    def step(i):
+        sample = timed["on"] and world > 1 and timed["i"] % KSAMPLE == 0
+        if sample:
+            marks[timed["n"]][0].record(stream)
+        if world > 1:
+            exchange_halo(srcs[i % NBUF], geo)
+        if sample:
+            marks[timed["n"]][1].record(stream)
+        run(i)
+        if sample:
+            marks[timed["n"]][2].record(stream)
+            timed["n"] += 1
+        if timed["on"]:
+            timed["i"] += 1
 
     for i in range(args.warmup):
         step(i)
@@ -268,8 +323,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    if cfg["kind"] != "texture":
-        timed["on"] = True
+    timed["on"] = True
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -281,15 +335,19 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if cfg["kind"] != "texture" and timed["n"] > 0:
+    exchange_ms = None
+    if timed["n"] > 0:
         n = timed["n"]
-        kernel_ms = sum(a.elapsed_time(b) for a, b in zip(kstart[:n], kend[:n])) / n
+        exchange_ms = sum(m[0].elapsed_time(m[1]) for m in marks[:n]) / n
+        kernel_ms = sum(m[1].elapsed_time(m[2]) for m in marks[:n]) / n
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    t = torch.tensor([elapsed, kernel_ms, exchange_ms or 0.0], dtype=torch.float64,
+                     device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kernel_ms = float(t[0]), float(t[1])
+    exchange_ms = float(t[2]) if world > 1 else None
 
     px_per_rank = rows * w
     total_px = px_per_rank * world if cfg["kind"] == "texture" or "rows_per_rank" in cfg else frame_h * w
@@ -343,6 +401,10 @@ def main():
                    "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
                    **({"backend": args.backend} if world > 1 else {})},
         "roofline": roof,
+        # per step, max over ranks: the kernel(s) and, at N>1, the halo exchange before
+        # them (event-timed on the filter stream every 4th step)
+        "kernel_ms": round(kernel_ms, 4),
+        **({"exchange_ms": round(exchange_ms, 4)} if exchange_ms is not None else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

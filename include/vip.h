@@ -85,10 +85,11 @@ int vip_joint_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_
                             size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, void* stream);
 /* Row-band variant for row-sharded frames (no reference counterpart; multi-GPU C5).
  * Filters `out_rows` rows of a handle-width image. Output row i is centred on source
- * row i + src_row0; neighbour rows are clamped to [row_lo, row_hi) of d_src (row_lo
- * may be negative-free halo bounds: rows below row_lo / above row_hi-1 replicate them,
- * which is exactly the reference's replicate border at the frame edges). d_guide may
- * be NULL (plain bilateral). */
+ * row i + src_row0; neighbour rows are clamped to [row_lo, row_hi) of d_src, with
+ * 0 <= row_lo < row_hi <= the handle's height (d_src and d_guide hold that many rows;
+ * rows below row_lo / above row_hi-1 replicate them, which is exactly the reference's
+ * replicate border at the frame edges). d_guide may be NULL (plain bilateral).
+ * Returns VIP_ERR_INVALID_ARGUMENT for a row range outside the handle's rows. */
 int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
                            size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, int out_rows, int src_row0,
                            int row_lo, int row_hi, void* stream);

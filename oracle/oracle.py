@@ -46,9 +46,10 @@ def lib() -> ctypes.CDLL:
         L.vipo_blur_rtv.argtypes = [vp, vp, vp, vp, i, i, i, i]
         L.vipo_guide.argtypes = [vp, vp, vp, i, i, i, i]
         L.vipo_texture.argtypes = [vp, vp, i, i, i, i, i]
+        L.vipo_set_variant.argtypes = [i]
         for fn in ("vipo_random_u8", "vipo_random_f32", "vipo_space_lut", "vipo_color_lut", "vipo_bilateral",
                    "vipo_bilateral_rows", "vipo_adaptive", "vipo_adaptive_rows", "vipo_gradient_u8",
-                   "vipo_gradient_f32", "vipo_blur_rtv", "vipo_guide", "vipo_texture"):
+                   "vipo_gradient_f32", "vipo_blur_rtv", "vipo_guide", "vipo_texture", "vipo_set_variant"):
             getattr(L, fn).restype = None
         _lib = L
     return _lib
@@ -57,6 +58,27 @@ def lib() -> ctypes.CDLL:
 def _p(a: np.ndarray) -> int:
     assert a.flags.c_contiguous
     return a.ctypes.data
+
+
+# ---- numerics-sensitivity variants of the CUDA profile (vip_oracle.c) ----
+V_SUMK_FMA, V_BLEND_B, V_BLEND_NO, V_EXP_UP, V_EXP_DOWN = 1, 2, 4, 8, 16
+VARIANTS = {"sumk_fma": V_SUMK_FMA, "blend_other_fma": V_BLEND_B, "blend_no_fma": V_BLEND_NO,
+            "exp_plus_1ulp": V_EXP_UP, "exp_minus_1ulp": V_EXP_DOWN}
+
+
+class variant:
+    """Context manager: CUDA-profile calls inside use the given variant flags
+    (process-global state of the oracle library; not thread-safe across variants)."""
+
+    def __init__(self, flags: int):
+        self.flags = flags
+
+    def __enter__(self):
+        lib().vipo_set_variant(self.flags)
+        return self
+
+    def __exit__(self, *exc):
+        lib().vipo_set_variant(0)
 
 
 # ---- inputs: test/random_array.hpp:9-31 ----
@@ -131,6 +153,40 @@ def bilateral_rows(src, row0, rows, ksize=9, sigma_space=10.0, sigma_color=30.0,
     dst = np.empty((rows, w, 3), np.uint8)
     lib().vipo_bilateral_rows(_p(src), None, _p(dst), w, h, ksize, sigma_space, sigma_color, profile, row0, rows)
     return dst
+
+
+def joint_bilateral_rows(src, guide, row0, rows, ksize=9, sigma_space=10.0, sigma_color=30.0, profile=CUDA):
+    src, guide = _img(src), _img(guide)
+    h, w, _ = src.shape
+    dst = np.empty((rows, w, 3), np.uint8)
+    lib().vipo_bilateral_rows(_p(src), _p(guide), _p(dst), w, h, ksize, sigma_space, sigma_color, profile, row0, rows)
+    return dst
+
+
+def adaptive_rows(src, row0, rows, ksize=9, sigma_space=10.0, sigma_color=30.0, profile=CUDA):
+    src = _img(src)
+    h, w, _ = src.shape
+    dst = np.empty((rows, w, 3), np.uint8)
+    lib().vipo_adaptive_rows(_p(src), _p(dst), w, h, ksize, sigma_space, sigma_color, profile, row0, rows)
+    return dst
+
+
+def texture_rows(src, row0, rows, ksize=9, nitr=3, profile=CUDA):
+    """Rows [row0, row0 + rows) of texture(src): the filter run on a crop with a
+    ghost margin of nitr * (halo of one iteration) rows on each side (clipped at the
+    frame edges, which are the crop's own edges there), so the band is exact."""
+    src = _img(src)
+    h = src.shape[0]
+    m = nitr * ((ksize - 1) + 2 * (ksize // 2) + 1)
+    a, b = max(0, row0 - m), min(h, row0 + rows + m)
+    return texture(src[a:b], ksize, nitr, profile)[row0 - a:row0 - a + rows]
+
+
+def bands(fn, spans, threads=8):
+    """[fn(row0, rows) for (row0, rows) in spans], evaluated in parallel threads
+    (the C calls release the GIL)."""
+    with ThreadPoolExecutor(min(threads, len(spans))) as ex:
+        return list(ex.map(lambda sp: fn(*sp), spans))
 
 
 def adaptive(src, ksize=9, sigma_space=10.0, sigma_color=30.0, profile=CUDA, threads=1):

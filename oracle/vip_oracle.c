@@ -31,6 +31,21 @@
 
 enum { VIPO_CUDA = 0, VIPO_CPP = 1 };
 
+/* Numerics-sensitivity variants of the CUDA profile (tests/test_oracle.py,
+ * scripts/numerics_sensitivity.py). Each bit replaces one code-generation choice
+ * that no reference artifact pins with the alternative nvcc could also have made;
+ * 0 (default) is the profile the HIP product reproduces bit for bit.
+ *   SUMK_FMA : sumk += ws * wc contracted to fmaf(ws, wc, sumk)
+ *              (src/bilateral_filter_impl.cu:84-89; the product also feeds the sums)
+ *   BLEND_B  : guide blend contracted the other way, fmaf(1-a, Bc, a * Bm)
+ *              (src/bilateral_texture_filter_impl.cu:168-176)
+ *   BLEND_NO : guide blend not contracted, a * Bm + (1-a) * Bc
+ *   EXP_UP / EXP_DOWN : the guide's exp one ulp above / below the correctly
+ *              rounded value (CUDA's expf is accurate to 2 ulp, not correctly rounded) */
+enum { VIPO_V_SUMK_FMA = 1, VIPO_V_BLEND_B = 2, VIPO_V_BLEND_NO = 4, VIPO_V_EXP_UP = 8, VIPO_V_EXP_DOWN = 16 };
+static int g_variant = 0;
+void vipo_set_variant(int flags) { g_variant = flags; }
+
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 /* float -> uint8 as static_cast<uint8_t>(v) does for v in [0,256); NaN (0/0 when
@@ -146,7 +161,10 @@ static void bilateral_rows(const uint8_t* src, const uint8_t* guide, uint8_t* ds
                     s0 = ACC(profile, s0, p[0], w);
                     s1 = ACC(profile, s1, p[1], w);
                     s2 = ACC(profile, s2, p[2], w);
-                    sk = sk + w;
+                    if (profile != VIPO_CPP && (g_variant & VIPO_V_SUMK_FMA))
+                        sk = fmaf(space[(ky + radius) * ksize + (kx + radius)], color[d], sk);
+                    else
+                        sk = sk + w;
                 }
             }
             uint8_t* o = dst + ((size_t)yy * width + x) * 3;
@@ -175,7 +193,7 @@ void vipo_bilateral(const uint8_t* src, const uint8_t* guide, uint8_t* dst, int 
 /* ------------------------------------------------------------------------- */
 /* Adaptive bilateral.                                                        */
 /*  CUDA: src/adaptive_bilateral_filter_impl.cu:7-115 (LUT of 512*3, :5)      */
-/*  CPP : include/cpp/adaptive_bilateral_filter.hpp:237-328                   */
+/*  CPP : include/cpp/adaptive_bilateral_filter.hpp:13-104                    */
 /* offset_c = ctr_c - boxsum_c / k^2 over the full k x k square (exact int    */
 /* sum either way, float divide); d = |n0-c0-o0| + |n1-c1-o1| + |n2-c2-o2| in */
 /* float, LUT index int(d) (truncation); weights use the circular space LUT.  */
@@ -218,7 +236,10 @@ void vipo_adaptive_rows(const uint8_t* src, uint8_t* dst, int width, int height,
                     s0 = ACC(profile, s0, p[0], w);
                     s1 = ACC(profile, s1, p[1], w);
                     s2 = ACC(profile, s2, p[2], w);
-                    sk = sk + w;
+                    if (profile != VIPO_CPP && (g_variant & VIPO_V_SUMK_FMA))
+                        sk = fmaf(space[(ky + radius) * ksize + (kx + radius)], color[(int)dist], sk);
+                    else
+                        sk = sk + w;
                 }
             }
             uint8_t* o = dst + ((size_t)yy * width + x) * 3;
@@ -360,7 +381,9 @@ void vipo_guide(const float* blurred, const float* rtv, uint8_t* guide, int widt
                 }
             }
             const float arg = sigma_alpha * (rtv[(size_t)y * width + x] - rtv[(size_t)my * width + mx]);
-            const float e = (float)exp((double)arg);
+            float e = (float)exp((double)arg);
+            if (profile != VIPO_CPP && (g_variant & VIPO_V_EXP_UP)) e = nextafterf(e, INFINITY);
+            if (profile != VIPO_CPP && (g_variant & VIPO_V_EXP_DOWN)) e = nextafterf(e, 0.f);
             const float alpha = 2.f / (1.f + e) - 1.f;
             const float beta = 1.f - alpha;
             const float* bm = blurred + ((size_t)my * width + mx) * 3;
@@ -368,7 +391,8 @@ void vipo_guide(const float* blurred, const float* rtv, uint8_t* guide, int widt
             uint8_t* g = guide + ((size_t)y * width + x) * 3;
             for (int c = 0; c < 3; c++) {
                 float v;
-                if (profile == VIPO_CPP) v = alpha * bm[c] + beta * bc[c] + 0.5f;
+                if (profile == VIPO_CPP || (g_variant & VIPO_V_BLEND_NO)) v = alpha * bm[c] + beta * bc[c] + 0.5f;
+                else if (g_variant & VIPO_V_BLEND_B) v = fmaf(beta, bc[c], alpha * bm[c]) + 0.5f;
                 else v = fmaf(alpha, bm[c], beta * bc[c]) + 0.5f;
                 g[c] = (uint8_t)clampi((int)v, 0, 255);
             }

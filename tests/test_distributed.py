@@ -62,6 +62,7 @@ def _worker(rank, world, port, width, height, ksize, kind, nitr, out_dir):
 
 
 @pytest.mark.parametrize("world,height,ksize,kind,nitr", [(2, 37, 9, "bilateral", 0), (3, 50, 15, "bilateral", 0),
+                                                          (2, 31, 31, "bilateral", 0),  # uneven 16/15-row shards, r=15
                                                           (2, 41, 7, "adaptive", 0), (2, 70, 5, "texture", 3),
                                                           (3, 90, 3, "texture", 4)])
 def test_row_sharded_halo_exchange_matches_full_frame(tmp_path, world, height, ksize, kind, nitr):
@@ -95,3 +96,15 @@ def test_shard_rows_partition():
     assert g.clamp_range() == (15, 15 + 2048 + 15) and g.slab_rows == 2048 + 30
     g = SlabGeometry(3840, 16384, 15, 7, 8)
     assert g.clamp_range() == (0, 15 + 2048)
+
+
+def test_thin_shards_rejected_on_every_rank():
+    """A halo deeper than the thinnest shard raises at construction on EVERY rank
+    (the same frame_height // world test everywhere), before any P2P call: uneven
+    shards must not let some ranks enter the exchange while others raise."""
+    from various_image_processings_amd.sharded import SlabGeometry
+    for rank in range(2):
+        with pytest.raises(ValueError):
+            SlabGeometry(64, 29, 15, rank, 2)  # shards of 15 and 14 rows, halo 15
+    SlabGeometry(64, 30, 15, 1, 2)  # 15 / 15: fine
+    SlabGeometry(64, 5, 15, 0, 1)   # one rank: no halo exchange

@@ -74,12 +74,16 @@ def test_joint_bilateral(dev, oracle, k, numerics, profile):
 
 @pytest.mark.parametrize("k", [9, 25])
 def test_joint_bilateral_multi_tile(dev, oracle, k):
-    # several persistent tiles per workgroup in both directions (joint kernel: 2 planes)
-    img = oracle.random_image(700, 530)
-    guide = oracle.random_u8(700 * 530 * 3)[::-1].copy().reshape(530, 700, 3)
+    # 3000 x 700: 24 x 11 = 264 (P=8) or 47 x 11 = 517 (P=4) tiles for 256 persistent
+    # workgroups -- several tiles per workgroup (next-tile prefetch and commit, the
+    # XCD tile permutation); ragged right and bottom edges
+    img = oracle.random_image(3000, 700)
+    guide = np.ascontiguousarray(img[::-1])
     got = _bilateral_gpu(dev, img, k, guide=guide)
-    want = oracle.joint_bilateral(img, guide, k, threads=8)
-    assert np.array_equal(got, want), _mismatch(got, want)
+    spans = [(0, 8), (60, 8), (380, 8), (692, 8)]
+    want = oracle.bands(lambda r0, n: oracle.joint_bilateral_rows(img, guide, r0, n, k), spans)
+    for (r0, n), w_ in zip(spans, want):
+        assert np.array_equal(got[r0:r0 + n], w_), (r0, _mismatch(got[r0:r0 + n], w_))
 
 
 @pytest.mark.parametrize("k", [3, 9, 15, 17, 31])
@@ -96,16 +100,20 @@ def test_adaptive(dev, oracle, k, numerics, profile):
 
 @pytest.mark.parametrize("k", [5, 15, 17, 19])
 def test_adaptive_multi_tile(dev, oracle, k):
-    # several persistent tiles per workgroup, ragged edges; k <= 17 takes the separable
-    # box-sum path (17: R|B sums unpacked before the horizontal windows), 19 the
-    # per-thread square sums
-    img = oracle.random_image(701, 331)
+    # 3000 x 701: 47 x 11 = 517 tiles of 64 x 64 for 256 persistent workgroups, so
+    # every workgroup runs the next-tile prefetch/commit and reuses its LDS sums;
+    # ragged edges. k <= 17 takes the separable box-sum path (17: R|B sums unpacked
+    # before the horizontal windows), 19 the per-thread square sums
+    img = oracle.random_image(3000, 701)
     h, w, _ = img.shape
     f = vip.CudaAdaptiveBilateralFilter(w, h, k)
     d_dst = dev.empty((h, w, 3))
     f.execute(dev.put(img), d_dst)
-    got, want = dev.get(d_dst), oracle.adaptive(img, k, threads=16)
-    assert np.array_equal(got, want), _mismatch(got, want)
+    got = dev.get(d_dst)
+    spans = [(0, 8), (60, 8), (380, 8), (693, 8)]
+    want = oracle.bands(lambda r0, n: oracle.adaptive_rows(img, r0, n, k), spans)
+    for (r0, n), w_ in zip(spans, want):
+        assert np.array_equal(got[r0:r0 + n], w_), (r0, _mismatch(got[r0:r0 + n], w_))
 
 
 def test_adaptive_natural_image(dev, oracle, lenna):
@@ -240,14 +248,36 @@ def test_full_4k_frame_rows_exact(dev, oracle):
         assert np.array_equal(got[r0:r0 + rows], want), (r0, _mismatch(got[r0:r0 + rows], want))
 
 
-def test_profiles_within_reference_tolerance(dev, oracle, lenna):
-    """GPU CUDA-profile output vs the include/cpp restatement: within the reference
-    tests' +-1 (EXPECT_NEAR(...,1)); report the exact-match fraction."""
-    got = _bilateral_gpu(dev, lenna, 15, numerics=0).astype(int)
-    want = oracle.bilateral(lenna, 15, profile=1, threads=16).astype(int)
-    diff = np.abs(got - want)
-    assert diff.max() <= 1
-    print(f"exact-match fraction vs include/cpp numerics: {(diff == 0).mean():.6f}")
+@pytest.mark.parametrize("image", ["random_array_50x50", "lenna"])
+def test_profiles_within_reference_tolerance(dev, oracle, lenna, image):
+    """GPU output (default CUDA numerics) vs the include/cpp restatement (oracle CPP
+    profile) for every filter: within the reference tests' +-1
+    (test/bilateral_filter.cu:58-60) for bilateral / joint / adaptive, and <= 1 on
+    >= 99.9 % of channels for the iterated texture filter. Prints
+    max |delta| and the exact-match percentage (table: DESIGN.md section 2)."""
+    img = oracle.random_image(50, 50) if image != "lenna" else lenna
+    h, w, _ = img.shape
+    guide = np.ascontiguousarray(img[::-1, ::-1])
+    d_src, d_dst = dev.put(img), dev.empty(img.shape)
+    runs = {
+        "bilateral k15": (lambda: vip.CudaBilateralFilter(w, h, 15).bilateral_filter(d_src, d_dst),
+                          lambda: oracle.bilateral(img, 15, profile=1, threads=16)),
+        "joint k9": (lambda: vip.CudaBilateralFilter(w, h, 9).joint_bilateral_filter(d_src, dev.put(guide), d_dst),
+                     lambda: oracle.joint_bilateral(img, guide, 9, profile=1, threads=16)),
+        "adaptive k15": (lambda: vip.CudaAdaptiveBilateralFilter(w, h, 15).execute(d_src, d_dst),
+                         lambda: oracle.adaptive(img, 15, profile=1, threads=16)),
+        "texture k5 nitr5": (lambda: vip.CudaBilateralTextureFilter(w, h, 5, 5).execute(d_src, d_dst),
+                             lambda: oracle.texture(img, 5, 5, profile=1)),
+    }
+    for name, (gpu, cpp) in runs.items():
+        gpu()
+        diff = np.abs(dev.get(d_dst).astype(int) - cpp().astype(int))
+        print(f"{image} {name}: max |delta| {diff.max()}, exact {(diff == 0).mean() * 100:.5f} %, "
+              f"<=1 {(diff <= 1).mean() * 100:.5f} %")
+        if name.startswith("texture"):
+            assert (diff <= 1).mean() >= 0.999, name
+        else:
+            assert diff.max() <= 1, name
 
 
 def test_host_frame_async_path(dev, oracle):

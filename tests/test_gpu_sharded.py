@@ -57,6 +57,7 @@ def _worker(rank, world, port, width, height, ksize, kind, nitr, out_dir):
     (3, 257, 140, 31, "bilateral", 0),
     (2, 190, 121, 15, "adaptive", 0),
     (2, 211, 150, 5, "texture", 3),
+    (8, 613, 400, 31, "bilateral", 0),  # C5's 8-way split (r=15) with a real gloo exchange
 ])
 def test_sharded_hip_kernels_match_full_frame(tmp_path, world, width, height, ksize, kind, nitr):
     import torch.multiprocessing as mp

@@ -5,7 +5,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 
 
 @pytest.mark.parametrize("name,kind,n,mx", [
@@ -201,3 +201,40 @@ def test_constant_division_is_exact():
         q0 = (s * rd).astype(np.float32)
         q = _fma32(_fma32(-q0, d32, s), rd, q0)
         assert np.array_equal(q, (s / d32).astype(np.float32)), d
+
+
+def test_numerics_sensitivity_within_reference_tolerance():
+    """The unpinned CUDA-profile choices (sumk add, guide-blend contraction, exp
+    rounding -- oracle.VARIANTS) and the include/cpp numerics move the outputs by at
+    most the reference tests' +-1 (test/bilateral_filter.cu:58-60) for the
+    bilateral, joint and adaptive filters; the texture filter ("<= 1 on
+    >= 99.9 %") stays within 1 on >= 99.9 % of channels. scripts/numerics_sensitivity.py
+    writes the full table (profiles/r02_numerics_sensitivity.json)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("ns", os.path.join(ROOT, "scripts", "numerics_sensitivity.py"))
+    ns = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ns)
+    from oracle import oracle as o
+    for name, fn in ns.cases().items():
+        base = fn(o.CUDA)
+        alts = [("cpp", fn(o.CPP))]
+        for vname, flags in o.VARIANTS.items():
+            if vname.startswith(("blend", "exp")) and not name.startswith("texture"):
+                continue
+            with o.variant(flags):
+                alts.append((vname, fn(o.CUDA)))
+        for vname, alt in alts:
+            s = ns.stats(alt, base)
+            if name.startswith("texture"):
+                assert s["within1_pct"] >= 99.9, (name, vname, s)
+            else:
+                assert s["max_abs"] <= 1, (name, vname, s)
+
+
+def test_texture_rows_band_equals_full_frame(oracle):
+    """oracle.texture_rows (a crop with an nitr * halo ghost margin) == those rows of
+    the full-frame filter: the full-size GPU texture test relies on it."""
+    img = oracle.random_image(61, 140)
+    full = oracle.texture(img, 5, 3)
+    for r0, n in ((0, 7), (50, 11), (131, 9)):
+        assert np.array_equal(oracle.texture_rows(img, r0, n, 5, 3), full[r0:r0 + n])

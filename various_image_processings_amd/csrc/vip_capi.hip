@@ -210,7 +210,10 @@ int vip_bilateral_destroy(vip_bilateral_t h) {
 int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
                            size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, int out_rows, int src_row0,
                            int row_lo, int row_hi, void* stream) {
-    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+    // d_src (and d_guide) hold the handle's height rows: every read clamps into
+    // [row_lo, row_hi), so that range must lie inside them
+    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi)
+        return VIP_ERR_INVALID_ARGUMENT;
     if (d_dst == d_src || (d_guide && d_dst == d_guide)) return VIP_ERR_ALIASING;
     const bool joint = d_guide != nullptr;
     StencilArgs a;
@@ -265,7 +268,8 @@ int vip_adaptive_destroy(vip_adaptive_t h) {
 
 int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
                           int out_rows, int src_row0, int row_lo, int row_hi, void* stream) {
-    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+    if (!h || !d_src || !d_dst || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi)
+        return VIP_ERR_INVALID_ARGUMENT;
     if (d_dst == d_src) return VIP_ERR_ALIASING;
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo, row_hi,

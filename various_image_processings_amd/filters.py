@@ -32,18 +32,34 @@ __all__ = [
 ]
 
 
-def _ptr(buf) -> int:
-    """Device address of a torch tensor (checked dense) or an int address."""
+def _ptr(buf, nbytes: int = 0, dtype: str = "uint8") -> int:
+    """Device address of a dense device buffer holding at least `nbytes` of `dtype`.
+
+    Accepts a torch tensor on the current HIP device (checked: device, density,
+    dtype, size -- a wrong-shaped tensor must raise here, not fault the GPU), a
+    DeviceImage (size checked), or a raw int address (unchecked: the caller's
+    responsibility, as in the reference's pointer API)."""
     if isinstance(buf, int):
         return buf
+    if isinstance(buf, DeviceImage):
+        if buf.nbytes < nbytes:
+            raise ValueError(f"DeviceImage of {buf.nbytes} bytes, {nbytes} needed")
+        return buf.get()
     if hasattr(buf, "data_ptr"):
         if not buf.is_cuda:
             raise ValueError("expected a device tensor (torch.cuda / HIP), got a host tensor")
+        import torch
+        if buf.device.index != torch.cuda.current_device():
+            raise ValueError(f"tensor on {buf.device}, but the current device is cuda:{torch.cuda.current_device()}")
         if not buf.is_contiguous():
             raise ValueError("expected a dense (contiguous) tensor")
+        want = {"uint8": torch.uint8, "float32": torch.float32}[dtype]
+        if buf.dtype != want:
+            raise ValueError(f"expected a {dtype} tensor, got {buf.dtype}")
+        have = buf.numel() * buf.element_size()
+        if have < nbytes:
+            raise ValueError(f"tensor of {have} bytes, {nbytes} needed ({tuple(buf.shape)})")
         return buf.data_ptr()
-    if isinstance(buf, DeviceImage):
-        return buf.get()
     raise TypeError(f"cannot take a device pointer of {type(buf).__name__}")
 
 
@@ -88,19 +104,21 @@ class _BilateralImpl(_Handle):
              float(sigma_space), float(sigma_color), int(numerics))
 
     def bilateral_filter(self, d_src, d_dst, stream=None):
-        p = self.width * 3
-        call("vip_bilateral_run", self._h, _ptr(d_src), p, _ptr(d_dst), p, _stream(stream))
+        p, n = self.width * 3, self.width * 3 * self.height
+        call("vip_bilateral_run", self._h, _ptr(d_src, n), p, _ptr(d_dst, n), p, _stream(stream))
 
     def joint_bilateral_filter(self, d_src, d_guide, d_dst, stream=None):
-        p = self.width * 3
-        call("vip_joint_bilateral_run", self._h, _ptr(d_src), p, _ptr(d_guide), p, _ptr(d_dst), p, _stream(stream))
+        p, n = self.width * 3, self.width * 3 * self.height
+        call("vip_joint_bilateral_run", self._h, _ptr(d_src, n), p, _ptr(d_guide, n), p, _ptr(d_dst, n), p,
+             _stream(stream))
 
     def run_rows(self, d_src, d_dst, out_rows, src_row0, row_lo, row_hi, d_guide=None, stream=None):
-        """Row-band filter for row-sharded frames (include/vip.h vip_bilateral_run_rows)."""
+        """Row-band filter for row-sharded frames (include/vip.h vip_bilateral_run_rows):
+        d_src (and d_guide) hold rows [0, row_hi) at least, d_dst out_rows rows."""
         p = self.width * 3
-        g = None if d_guide is None else _ptr(d_guide)
-        call("vip_bilateral_run_rows", self._h, _ptr(d_src), p, g, p, _ptr(d_dst), p, int(out_rows), int(src_row0),
-             int(row_lo), int(row_hi), _stream(stream))
+        g = None if d_guide is None else _ptr(d_guide, p * int(row_hi))
+        call("vip_bilateral_run_rows", self._h, _ptr(d_src, p * int(row_hi)), p, g, p, _ptr(d_dst, p * int(out_rows)),
+             p, int(out_rows), int(src_row0), int(row_lo), int(row_hi), _stream(stream))
 
 
 class CudaBilateralFilter:
@@ -129,13 +147,13 @@ class _AdaptiveImpl(_Handle):
              float(sigma_space), float(sigma_color), int(numerics))
 
     def execute(self, d_src, d_dst, stream=None):
-        p = self.width * 3
-        call("vip_adaptive_run", self._h, _ptr(d_src), p, _ptr(d_dst), p, _stream(stream))
+        p, n = self.width * 3, self.width * 3 * self.height
+        call("vip_adaptive_run", self._h, _ptr(d_src, n), p, _ptr(d_dst, n), p, _stream(stream))
 
     def run_rows(self, d_src, d_dst, out_rows, src_row0, row_lo, row_hi, stream=None):
         p = self.width * 3
-        call("vip_adaptive_run_rows", self._h, _ptr(d_src), p, _ptr(d_dst), p, int(out_rows), int(src_row0),
-             int(row_lo), int(row_hi), _stream(stream))
+        call("vip_adaptive_run_rows", self._h, _ptr(d_src, p * int(row_hi)), p, _ptr(d_dst, p * int(out_rows)), p,
+             int(out_rows), int(src_row0), int(row_lo), int(row_hi), _stream(stream))
 
 
 class CudaAdaptiveBilateralFilter:
@@ -160,20 +178,25 @@ class _TextureImpl(_Handle):
              int(numerics))
 
     def execute(self, d_src, d_dst, stream=None):
-        call("vip_texture_run", self._h, _ptr(d_src), _ptr(d_dst), _stream(stream))
+        n = self.width * self.height * 3
+        call("vip_texture_run", self._h, _ptr(d_src, n), _ptr(d_dst, n), _stream(stream))
 
     def compute_blur_and_rtv(self, d_image, d_magnitude, d_blurred, d_rtv, stream=None):
-        call("vip_texture_blur_rtv", self._h, _ptr(d_image), _ptr(d_magnitude), _ptr(d_blurred), _ptr(d_rtv),
-             _stream(stream))
+        n = self.width * self.height
+        call("vip_texture_blur_rtv", self._h, _ptr(d_image, 3 * n), _ptr(d_magnitude, 4 * n, "float32"),
+             _ptr(d_blurred, 12 * n, "float32"), _ptr(d_rtv, 4 * n, "float32"), _stream(stream))
 
     def compute_guide(self, d_blurred, d_rtv, d_guide, stream=None):
-        call("vip_texture_guide", self._h, _ptr(d_blurred), _ptr(d_rtv), _ptr(d_guide), _stream(stream))
+        n = self.width * self.height
+        call("vip_texture_guide", self._h, _ptr(d_blurred, 12 * n, "float32"), _ptr(d_rtv, 4 * n, "float32"),
+             _ptr(d_guide, 3 * n), _stream(stream))
 
     def iterate_rows(self, d_src, d_dst, out_row0, out_rows, row_lo, row_hi, stream=None):
         """One iteration on a row slab (include/vip.h vip_texture_iterate_rows): d_dst
         receives slab rows [out_row0, out_row0 + out_rows)."""
-        call("vip_texture_iterate_rows", self._h, _ptr(d_src), _ptr(d_dst), self.width * 3, int(out_row0),
-             int(out_rows), int(row_lo), int(row_hi), _stream(stream))
+        p = self.width * 3
+        call("vip_texture_iterate_rows", self._h, _ptr(d_src, p * self.height), _ptr(d_dst, p * int(out_rows)), p,
+             int(out_row0), int(out_rows), int(row_lo), int(row_hi), _stream(stream))
 
 
 class CudaBilateralTextureFilter:
@@ -193,7 +216,9 @@ def cuda_gradient(d_src, d_dst, width, height, src_ch=1, numerics=VIP_NUMERICS_C
     Asynchronous, like src/gradient_impl.cu:90-103."""
     is_f32 = hasattr(d_src, "dtype") and str(d_src.dtype) == "torch.float32"
     name = "vip_gradient_f32" if is_f32 else "vip_gradient_u8"
-    call(name, _ptr(d_src), _ptr(d_dst), int(width), int(height), int(src_ch), int(numerics), _stream(stream))
+    n = int(width) * int(height)
+    call(name, _ptr(d_src, n * int(src_ch) * (4 if is_f32 else 1), "float32" if is_f32 else "uint8"),
+         _ptr(d_dst, 4 * n, "float32"), int(width), int(height), int(src_ch), int(numerics), _stream(stream))
 
 
 class DeviceImage:

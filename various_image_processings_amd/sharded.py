@@ -38,6 +38,17 @@ class SlabGeometry:
     rank: int
     world: int
 
+    def __post_init__(self):
+        # Checked identically on every rank, before any P2P call: the thinnest shard
+        # (shard_rows gives sizes that differ by one) must still cover a full halo,
+        # or the ranks whose shards are thick enough would block in the exchange
+        # while the others raise.
+        if not (0 <= self.rank < self.world):
+            raise ValueError(f"rank {self.rank} outside world {self.world}")
+        if self.world > 1 and self.radius > 0 and self.frame_height // self.world < self.radius:
+            raise ValueError(f"{self.frame_height} rows over {self.world} ranks: the thinnest shard "
+                             f"({self.frame_height // self.world} rows) is thinner than the {self.radius}-row halo")
+
     @property
     def rows(self) -> tuple[int, int]:
         return shard_rows(self.frame_height, self.world, self.rank)
@@ -79,8 +90,6 @@ def exchange_halo(slab, geo: SlabGeometry, group=None) -> None:
     r, n = geo.radius, geo.own
     if geo.world == 1 or r == 0:
         return
-    if n < r:
-        raise ValueError(f"shard of {n} rows is thinner than the halo ({r} rows)")
     # gloo moves host tensors only: a device slab is staged through host copies
     # (CPU rehearsal of the N>1 path; with nccl = RCCL the slab rows go GPU to GPU)
     staged = slab.is_cuda and dist.get_backend(group) == "gloo"
@@ -124,6 +133,23 @@ def exchange_halo(slab, geo: SlabGeometry, group=None) -> None:
             dst.copy_(host)
 
 
+def _exchange_on(slab, geo: SlabGeometry, stream) -> None:
+    """exchange_halo ordered before later work on `stream`.
+
+    With RCCL, a request's wait() orders the received rows only before torch's
+    CURRENT stream; the kernel that reads them runs on `stream` (a torch.cuda.Stream,
+    a raw hipStream_t address, or None = the current stream), so the exchange runs
+    with `stream` made current.
+    """
+    if stream is None:
+        exchange_halo(slab, geo)
+        return
+    import torch
+    s = stream if isinstance(stream, torch.cuda.Stream) else torch.cuda.ExternalStream(int(stream), device=slab.device)
+    with torch.cuda.stream(s):
+        exchange_halo(slab, geo)
+
+
 class ShardedBilateral:
     """Bilateral (or adaptive) filter of a row-sharded frame on the HIP kernels."""
 
@@ -139,7 +165,7 @@ class ShardedBilateral:
     def filter(self, slab, out, stream=None, exchange: bool = True) -> None:
         """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3)."""
         if exchange:
-            exchange_halo(slab, self.geo)
+            _exchange_on(slab, self.geo, stream)
         lo, hi = self.geo.clamp_range()
         self.impl.run_rows(slab, out, self.geo.own, self.geo.radius, lo, hi, stream=stream)
 
@@ -176,7 +202,7 @@ class ShardedTexture:
         import torch
         g = self.geo
         if exchange:
-            exchange_halo(slab, g)
+            _exchange_on(slab, g, stream)
         if self.nitr == 0:
             out.copy_(slab[g.radius:g.radius + g.own])
             return
