@@ -24,15 +24,17 @@ namespace vip {
 
 // Separable box sums need VRB (TH x VW words) after the plane and VW u16 of VG in each
 // plane row's unused tail (S - VW words): true up to R = 8 at 16 waves.
-template <int R, int P, int WAVES>
+template <int R, int P, int WAVES, int LUTW = lut_words(true)>
 constexpr bool adaptive_vbox() {
     using G = Geom<R, P>;
     constexpr int VW = G::GROUPS * 4;
-    return VW <= 2 * (G::S - VW) &&
-           lds_bytes<R, WAVES, 1, lut_words(true), P>() + 4LL * (WAVES * 4) * VW <= kLdsBudget;
+    return VW <= 2 * (G::S - VW) && lds_bytes<R, WAVES, 1, LUTW, P>() + 4LL * (WAVES * 4) * VW <= kLdsBudget;
 }
 
-template <int R, int WAVES, bool FMA, int P>
+// NE: LUT entries in LDS (1536 x 16 copies; or 512 x 32 copies, bank-conflict free, when
+// the colour LUT is exactly zero from entry 511 on -- sigma_color 30 underflows past
+// d = 431 -- with the index clamped to 511: one v_min_u32 per tap).
+template <int R, int WAVES, bool FMA, int P, int NE = 1536>
 __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
@@ -48,13 +50,14 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     // the plane rows' unused tail words), then each thread slides its K-column windows
     // over them. Fits the LDS for R <= 8; larger radii keep the per-thread square sums.
     constexpr int VW = G::GROUPS * 4;          // plane words in use per row (TW + 2L)
-    constexpr bool VBOX = adaptive_vbox<R, P, WAVES>();
+    constexpr bool VBOX = adaptive_vbox<R, P, WAVES, NE * (NE < 1536 ? 32 : 16)>();
     // straight-line rows where the separable box sums apply (R <= 8); the larger
     // radii keep the row loop (code size and build time)
     constexpr bool ROW_UNROLL = VIP_ADA_UNROLL != 0 && VBOX;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
-    uint32_t* const plane = lds + lut_words(true);
+    constexpr int COPIES = NE < 1536 ? 32 : 16;
+    uint32_t* const plane = lds + NE * COPIES;
     uint32_t* const vrb = plane + ROWS * G::S;  // VBOX: TH x VW words
 
     const int tid = threadIdx.x;
@@ -62,7 +65,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int tx = lane & 15;
     const int ty = wave * 4 + (lane >> 4);
-    const uint32_t lane16 = (uint32_t)(lane & 15) << 2;
+    const uint32_t lane16 = (uint32_t)(lane & (COPIES - 1)) << 2;
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x
@@ -71,7 +74,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
         const int mt = xcd_tile(tile, a.tiles_total);
         pf.issue(a.src, a.src_pitch, a, (mt % a.tiles_x) * G::TW, (mt / a.tiles_x) * TH);
     }
-    stage_lut<NT, 1536, 16>(lut, a.color);
+    stage_lut<NT, NE, COPIES>(lut, a.color);
     pf.commit(plane);
     __syncthreads();
 
@@ -258,7 +261,9 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                         const float d1 = (n01.y - c1f[i]) - o1[i];
                         const float d2 = (n21.x - c2f[i]) - o2[i];
                         const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
-                        return ((uint32_t)dist << 6) | lane16;
+                        uint32_t d = (uint32_t)dist;
+                        if constexpr (NE < 1536) d = d < NE - 1 ? d : NE - 1;
+                        return (d << (COPIES == 32 ? 7 : 6)) | lane16;
                     };
                     row_taps<HW, G::L, C0, NC, FMA, false, P, false>(plane, plane, row_off, wsv, lut_bytes, widx, a01,
                                                                      a2k);
@@ -277,19 +282,24 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     }
 }
 
-template <int R, bool FMA>
-static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
+#ifndef VIP_ADA_SHORT_LUT
+#define VIP_ADA_SHORT_LUT 0
+#endif
+
+template <int R, bool FMA, int NE>
+static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     // P = 8 outputs per thread needs ~170 VGPRs (per-output centre/offset floats,
     // accumulators, pipelined LUT reads) -> 8 waves; P = 4 fits 128 -> 16 waves
     constexpr int P = VIP_ADA_P;
     using G = Geom<R, P>;
-    constexpr int WAVES = pick_waves<R, 1, P == 8 ? 8 : 16, lut_words(true), P>();
+    constexpr int LUTW = NE * (NE < 1536 ? 32 : 16);
+    constexpr int WAVES = pick_waves<R, 1, P == 8 ? 8 : 16, LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, 1, lut_words(true), P>() +
-                        (adaptive_vbox<R, P, WAVES>() ? 4 * TH * G::GROUPS * 4 : 0);
+    constexpr int LDS = lds_bytes<R, WAVES, 1, LUTW, P>() +
+                        (adaptive_vbox<R, P, WAVES, LUTW>() ? 4 * TH * G::GROUPS * 4 : 0);
     static_assert(LDS <= kLdsBudget, "adaptive tile does not fit LDS");
-    auto kern = adaptive_kernel<R, WAVES, FMA, P>;
+    auto kern = adaptive_kernel<R, WAVES, FMA, P, NE>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
@@ -299,6 +309,13 @@ static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
     const int blocks = persistent_blocks(args.tiles_total);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
+}
+
+template <int R, bool FMA>
+static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
+    if constexpr (VIP_ADA_SHORT_LUT != 0)
+        if (a.lut_nonzero <= 511) return launch_adaptive_ne<R, FMA, 512>(a, stream);
+    return launch_adaptive_ne<R, FMA, 1536>(a, stream);
 }
 
 template <bool FMA>

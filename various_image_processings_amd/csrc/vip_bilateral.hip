@@ -46,7 +46,11 @@ __device__ __forceinline__ void vip_rt_stamp(int k) {
 #ifndef VIP_BIL_RCP  // epilogue: one exact reciprocal per output instead of 3 IEEE divides
 #define VIP_BIL_RCP 1
 #endif
-template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P>
+// NE: colour-LUT entries held in LDS. 768 (every L1 distance), or 32 when the
+// handle's LUT is exactly zero from entry 31 on (small sigma_color: the texture
+// filter's JBF has sigma_color sqrt(3), nonzero up to d = 24): the distance is then
+// clamped to 31 (one v_min_u32 per tap) and the 32-copy table takes 4 KiB.
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
@@ -56,7 +60,7 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     constexpr int PLANE = ROWS * G::S;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
-    uint32_t* const gplane = lds + 768 * COPIES;
+    uint32_t* const gplane = lds + NE * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
     const int tid = threadIdx.x;
@@ -77,7 +81,7 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
         pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
-    stage_lut<NT, 768, COPIES>(lut, a.color);  // once per workgroup
+    stage_lut<NT, NE, COPIES>(lut, a.color);  // once per workgroup
     pg.commit(gplane);
     if constexpr (JOINT) ps.commit(splane);
     __syncthreads();
@@ -120,7 +124,9 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
                     // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*COPIES + lane copy
                     auto widx = [&](uint32_t g, f2, f2, int i) {
-                        return (__builtin_amdgcn_sad_u8(g, ctr[i], 0u) << (COPIES == 32 ? 7 : 6)) | lane4;
+                        uint32_t d = __builtin_amdgcn_sad_u8(g, ctr[i], 0u);
+                        if constexpr (NE < 768) d = d < NE - 1 ? d : NE - 1;
+                        return (d << (COPIES == 32 ? 7 : 6)) | lane4;
                     };
                     row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT>(gplane, splane, row_off, wsv, lut_bytes, widx,
                                                                      a01, a2k);
@@ -175,16 +181,20 @@ constexpr int lut_copies() {
 template <int R, int PLANES>
 constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
 
-template <int R, bool JOINT, bool FMA>
-static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
+#ifndef VIP_JBF_SHORT_LUT  // joint kernel: 32-entry clamped LUT when the colour LUT allows it
+#define VIP_JBF_SHORT_LUT 0
+#endif
+
+template <int R, bool JOINT, bool FMA, int NE>
+static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
     constexpr int P = outputs_per_thread<R, PLANES>();
-    constexpr int COPIES = lut_copies<R, PLANES>();
-    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), 768 * COPIES, P>();
+    constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
+    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), NE * COPIES, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, PLANES, 768 * COPIES, P>();
-    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P>;
+    constexpr int LDS = lds_bytes<R, WAVES, PLANES, NE * COPIES, P>();
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
@@ -194,6 +204,13 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     const int blocks = persistent_blocks(args.tiles_total);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
+}
+
+template <int R, bool JOINT, bool FMA>
+static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
+    if constexpr (JOINT && VIP_JBF_SHORT_LUT)
+        if (a.lut_nonzero <= 31) return launch_bilateral_ne<R, JOINT, FMA, 32>(a, stream);
+    return launch_bilateral_ne<R, JOINT, FMA, 768>(a, stream);
 }
 
 template <bool JOINT, bool FMA>

@@ -67,9 +67,13 @@ static void build_color(int len, float sigma_color, int numerics, float* out) {
 
 static bool valid_ksize(int ksize) { return ksize >= 3 && (ksize & 1) && ksize / 2 <= kMaxRadius; }
 
-static int upload_color(float** d_color, int len, float sigma_color, int numerics) {
+// Returns the number of leading entries up to the last nonzero one in *nonzero.
+static int upload_color(float** d_color, int len, float sigma_color, int numerics, int* nonzero) {
     float host[1536];
     build_color(len, sigma_color, numerics, host);
+    int nz = len;
+    while (nz > 0 && host[nz - 1] == 0.f) --nz;
+    *nonzero = nz;
     VIP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(d_color), sizeof(float) * len));
     VIP_HIP_CHECK(hipMemcpy(*d_color, host, sizeof(float) * len, hipMemcpyHostToDevice));
     return 0;
@@ -77,7 +81,7 @@ static int upload_color(float** d_color, int len, float sigma_color, int numeric
 
 static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_pitch, const uint8_t* guide,
                       size_t guide_pitch, uint8_t* dst, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
-                      int row_hi, const float* d_color, const float* wsq) {
+                      int row_hi, const float* d_color, int lut_nonzero, const float* wsq) {
     a.src = src;
     a.guide = guide;
     a.dst = dst;
@@ -94,6 +98,7 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.aligned = al4(src, src_pitch) && al4(guide, guide_pitch);
     a.dst_aligned = ((uintptr_t)dst % 8 == 0) && (dst_pitch % 8 == 0);
     a.color = d_color;
+    a.lut_nonzero = lut_nonzero;
     std::memcpy(a.ws, wsq, sizeof(a.ws));
 }
 
@@ -102,13 +107,13 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
 using namespace vip;
 
 struct vip_bilateral_s {
-    int width, height, ksize, radius, numerics;
+    int width, height, ksize, radius, numerics, lut_nonzero;
     float* d_color;
     float wsq[kWsStride * kWsStride];
 };
 
 struct vip_adaptive_s {
-    int width, height, ksize, radius, numerics;
+    int width, height, ksize, radius, numerics, lut_nonzero;
     float* d_color;
     float wsq[kWsStride * kWsStride];
 };
@@ -191,7 +196,7 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
     h->radius = ksize / 2;
     h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
-    const int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics);
+    const int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics, &h->lut_nonzero);
     if (rc) {
         delete h;
         return rc;
@@ -218,7 +223,7 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
     const bool joint = d_guide != nullptr;
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, joint ? d_guide : d_src, joint ? guide_pitch : src_pitch, d_dst,
-              dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->wsq);
+              dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, h->wsq);
     return launch_bilateral(h->radius, joint, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
 }
 
@@ -250,7 +255,7 @@ int vip_adaptive_create(vip_adaptive_t* out, int width, int height, int ksize, f
     h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
     // the reference's table is 512*3 long (src/adaptive_bilateral_filter_impl.cu:5)
-    const int rc = upload_color(&h->d_color, 1536, sigma_color, h->numerics);
+    const int rc = upload_color(&h->d_color, 1536, sigma_color, h->numerics, &h->lut_nonzero);
     if (rc) {
         delete h;
         return rc;
@@ -273,7 +278,7 @@ int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pit
     if (d_dst == d_src) return VIP_ERR_ALIASING;
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo, row_hi,
-              h->d_color, h->wsq);
+              h->d_color, h->lut_nonzero, h->wsq);
     return launch_adaptive(h->radius, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
 }
 

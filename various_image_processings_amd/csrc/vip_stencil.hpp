@@ -39,6 +39,7 @@ struct StencilArgs {
     int aligned;           // src/guide base and pitch are 4-byte aligned -> dword tile loads
     int dst_aligned;       // dst base and pitch are 8-byte aligned -> qword stores
     const float* color;    // colour LUT in device memory
+    int lut_nonzero;       // entries [lut_nonzero, end) of the colour LUT are exactly 0
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 

@@ -262,7 +262,10 @@ namespace vip {
 #ifndef VIP_GF_TH
 #define VIP_GF_TH 16
 #endif
-constexpr int kGfTW = VIP_GF_TW, kGfTH = VIP_GF_TH, kGfNT = 256;
+#ifndef VIP_GF_NT
+#define VIP_GF_NT 256
+#endif
+constexpr int kGfTW = VIP_GF_TW, kGfTH = VIP_GF_TH, kGfNT = VIP_GF_NT;
 static_assert(kGfTW % 4 == 0 && kGfTH % 4 == 0, "guide tile: 4-pixel groups, 4-row runs");
 constexpr int kGfH1 = 8;   // pass 1: horizontally adjacent window aggregates per thread
 constexpr int kGfV2 = 4;   // pass 2: vertically adjacent blur positions per thread
