@@ -20,9 +20,12 @@ guide = srcs[5]
 cases = [("bilateral", _BilateralImpl(W, H, 15).bilateral_filter),
          ("adaptive", _AdaptiveImpl(W, H, 15).execute)]
 j9, j15 = _BilateralImpl(W, H, 9), _BilateralImpl(W, H, 15)
+jt = _BilateralImpl(W, H, 9, 4.0, 1.73205080757)  # the texture filter's JBF at k = 5
 cases += [("joint_r4", lambda s, d: j9.joint_bilateral_filter(s, guide, d)),
+          ("joint_r4_texture_sigmas", lambda s, d: jt.joint_bilateral_filter(s, guide, d)),
           ("joint_r7", lambda s, d: j15.joint_bilateral_filter(s, guide, d)),
-          ("texture_k5_nitr1", _TextureImpl(W, H, 5, 1).execute)]
+          ("texture_k5_nitr1", _TextureImpl(W, H, 5, 1).execute),
+          ("texture_k5_nitr5", _TextureImpl(W, H, 5, 5).execute)]
 if "--r15" in sys.argv:  # one 2048-row slab of the C5 frame (16384 wide, ksize 31)
     s15 = [torch.randint(0, 255, (2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     d15 = torch.empty((2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda")

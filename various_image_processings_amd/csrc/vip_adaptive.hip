@@ -253,7 +253,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
                     // dist = |(n0-c0)-o0| + |(n1-c1)-o1| + |(n2-c2)-o2|; (float)(n-c) == f_n - f_c exactly.
                     // Index int(dist) <= 1530 -> word d*16 + (lane & 15) of the 1536 x 16 LUT.
-                    auto widx = [&](uint32_t, f2 n01, f2 n21, int i) {
+                    auto widx = [&](uint32_t, f2 n01, f2 n21, int i, int) {
                         // scalar subtracts here and scalar fma accumulation (row_taps PK =
                         // false): the packed forms (v_pk_add_f32 {b, g} pairs, v_pk_fma_f32
                         // accumulation) measured 446 us per 4K frame against 381 us

@@ -50,7 +50,21 @@ __device__ __forceinline__ void vip_rt_stamp(int k) {
 // handle's LUT is exactly zero from entry 31 on (small sigma_color: the texture
 // filter's JBF has sigma_color sqrt(3), nonzero up to d = 24): the distance is then
 // clamped to 31 (one v_min_u32 per tap) and the 32-copy table takes 4 KiB.
-template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768>
+// FOLD (with NE = 32): one such table per distinct squared tap distance r^2, holding
+// the full weight RN(ws(r^2) * wc[d]) -- the same float product the unfolded taps
+// form, so bit-identical -- addressed by the tap's compile-time table offset (the
+// ds_read immediate): per tap v_sad_u8, v_min_u32, v_lshl_or, 3 v_fma, v_add and no
+// spatial v_mul; with 32 copies the reads are bank-conflict free. At R = 4 (the C4
+// JBF) 10 tables = 40 KiB, against 48 KiB for the 16-copy (2-way conflicting) LUT.
+template <int R>
+struct FoldRank {  // table index of tap (|ky|, |kx|)
+    int t[(R + 1) * (R + 1)];
+    constexpr FoldRank() : t() {
+        for (int y = 0; y <= R; ++y)
+            for (int x = 0; x <= R; ++x) t[y * (R + 1) + x] = disc_r2_rank(R, x * x + y * y);
+    }
+};
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false>
 __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
@@ -60,7 +74,9 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     constexpr int PLANE = ROWS * G::S;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
-    uint32_t* const gplane = lds + NE * COPIES;
+    constexpr int NTAB = FOLD ? disc_r2_count(R) : 1;
+    static_assert(!FOLD || (NE == 32 && COPIES == 32), "folded tables: 32 entries x 32 copies");
+    uint32_t* const gplane = lds + NTAB * NE * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
     const int tid = threadIdx.x;
@@ -81,7 +97,10 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
         pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
-    stage_lut<NT, NE, COPIES>(lut, a.color);  // once per workgroup
+    if constexpr (FOLD)
+        stage_lut<NT, NTAB * NE, COPIES>(lut, a.fold);  // once per workgroup
+    else
+        stage_lut<NT, NE, COPIES>(lut, a.color);
     pg.commit(gplane);
     if constexpr (JOINT) ps.commit(splane);
     __syncthreads();
@@ -123,13 +142,18 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
 #pragma unroll
                     for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
                     // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*COPIES + lane copy
-                    auto widx = [&](uint32_t g, f2, f2, int i) {
+                    auto widx = [&](uint32_t g, f2, f2, int i, int kx) {
                         uint32_t d = __builtin_amdgcn_sad_u8(g, ctr[i], 0u);
                         if constexpr (NE < 768) d = d < NE - 1 ? d : NE - 1;
-                        return (d << (COPIES == 32 ? 7 : 6)) | lane4;
+                        const uint32_t ad = (d << (COPIES == 32 ? 7 : 6)) | lane4;
+                        if constexpr (FOLD) {
+                            constexpr FoldRank<R> rank;
+                            return ad + (uint32_t)rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)] * (NE * COPIES * 4);
+                        }
+                        return ad;
                     };
-                    row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT>(gplane, splane, row_off, wsv, lut_bytes, widx,
-                                                                     a01, a2k);
+                    row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT, decltype(widx)&, FOLD>(
+                        gplane, splane, row_off, wsv, lut_bytes, widx, a01, a2k);
                     if constexpr (ROW_UNROLL) fence_accumulators(a01, a2k);
             });
 
@@ -185,16 +209,17 @@ constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
 #define VIP_JBF_SHORT_LUT 0
 #endif
 
-template <int R, bool JOINT, bool FMA, int NE>
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false>
 static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
     constexpr int P = outputs_per_thread<R, PLANES>();
     constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
-    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), NE * COPIES, P>();
+    constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
+    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, PLANES, NE * COPIES, P>();
-    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE>;
+    constexpr int LDS = lds_bytes<R, WAVES, PLANES, LUTW, P>();
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
@@ -208,6 +233,8 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
 
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
+    if constexpr (JOINT && R <= kFoldMaxR)
+        if (a.fold) return launch_bilateral_ne<R, JOINT, FMA, 32, true>(a, stream);
     if constexpr (JOINT && VIP_JBF_SHORT_LUT)
         if (a.lut_nonzero <= 31) return launch_bilateral_ne<R, JOINT, FMA, 32>(a, stream);
     return launch_bilateral_ne<R, JOINT, FMA, 768>(a, stream);

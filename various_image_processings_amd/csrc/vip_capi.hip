@@ -81,7 +81,7 @@ static int upload_color(float** d_color, int len, float sigma_color, int numeric
 
 static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_pitch, const uint8_t* guide,
                       size_t guide_pitch, uint8_t* dst, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
-                      int row_hi, const float* d_color, int lut_nonzero, const float* wsq) {
+                      int row_hi, const float* d_color, int lut_nonzero, const float* d_fold, const float* wsq) {
     a.src = src;
     a.guide = guide;
     a.dst = dst;
@@ -99,6 +99,7 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.dst_aligned = ((uintptr_t)dst % 8 == 0) && (dst_pitch % 8 == 0);
     a.color = d_color;
     a.lut_nonzero = lut_nonzero;
+    a.fold = d_fold;
     std::memcpy(a.ws, wsq, sizeof(a.ws));
 }
 
@@ -109,6 +110,7 @@ using namespace vip;
 struct vip_bilateral_s {
     int width, height, ksize, radius, numerics, lut_nonzero;
     float* d_color;
+    float* d_fold;  // joint kernel's folded tables (small sigma_color, radius <= kFoldMaxR), or null
     float wsq[kWsStride * kWsStride];
 };
 
@@ -184,6 +186,29 @@ int vip_stream_wait_event(void* stream, void* event) {
 int vip_event_synchronize(void* event) { return (int)hipEventSynchronize((hipEvent_t)event); }
 
 // ---------------------------------------------------------------- bilateral
+// Folded joint-kernel tables: table t (the t-th distinct r^2 of the disc, ascending)
+// entry d = RN(ws(r^2) * wc[d]) for d < 32 -- the product the kernel's unfolded taps
+// form (one float multiply), so results are unchanged. Needs wc[31..767] == 0.
+static int upload_fold(vip_bilateral_s* h, float sigma_color) {
+    const int R = h->radius;
+    float wc[768];
+    build_color(768, sigma_color, h->numerics, wc);
+    float fold[(kFoldMaxR * kFoldMaxR + 1) * 32];
+    int ntab = 0;
+    for (int v = 0; v <= R * R; ++v) {
+        if (!is_disc_r2(R, v)) continue;
+        float ws = 0.f;  // the spatial weight of any tap at squared distance v
+        for (int y = 0; y <= R; ++y)
+            for (int x = 0; x <= R; ++x)
+                if (x * x + y * y == v) ws = h->wsq[y * kWsStride + x];
+        for (int d = 0; d < 32; ++d) fold[ntab * 32 + d] = wc[d] * ws;
+        ++ntab;
+    }
+    VIP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->d_fold), sizeof(float) * 32 * ntab));
+    VIP_HIP_CHECK(hipMemcpy(h->d_fold, fold, sizeof(float) * 32 * ntab, hipMemcpyHostToDevice));
+    return 0;
+}
+
 int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
                          int numerics) {
     if (!out || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
@@ -196,9 +221,10 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
     h->radius = ksize / 2;
     h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
-    const int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics, &h->lut_nonzero);
+    int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics, &h->lut_nonzero);
+    if (!rc && h->lut_nonzero <= 31 && h->radius <= kFoldMaxR) rc = upload_fold(h, sigma_color);
     if (rc) {
-        delete h;
+        vip_bilateral_destroy(h);
         return rc;
     }
     *out = h;
@@ -207,7 +233,8 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
 
 int vip_bilateral_destroy(vip_bilateral_t h) {
     if (!h) return 0;
-    const int rc = (int)hipFree(h->d_color);
+    if (h->d_fold) (void)hipFree(h->d_fold);
+    const int rc = h->d_color ? (int)hipFree(h->d_color) : 0;
     delete h;
     return rc;
 }
@@ -223,7 +250,8 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
     const bool joint = d_guide != nullptr;
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, joint ? d_guide : d_src, joint ? guide_pitch : src_pitch, d_dst,
-              dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, h->wsq);
+              dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, joint ? h->d_fold : nullptr,
+              h->wsq);
     return launch_bilateral(h->radius, joint, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
 }
 
@@ -278,7 +306,7 @@ int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pit
     if (d_dst == d_src) return VIP_ERR_ALIASING;
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo, row_hi,
-              h->d_color, h->lut_nonzero, h->wsq);
+              h->d_color, h->lut_nonzero, nullptr, h->wsq);
     return launch_adaptive(h->radius, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
 }
 

@@ -36,6 +36,22 @@ __host__ __device__ constexpr int isqrt_floor(int v) {
 }
 __host__ __device__ constexpr int circle_hw(int R, int ky) { return isqrt_floor(R * R - ky * ky); }
 
+// Distinct squared tap distances v = kx^2 + ky^2 <= R^2 of the disc (0 <= kx, ky <= R),
+// ranked in ascending order: the folded colour x space LUT of the bilateral kernel
+// holds one table per distinct v.
+__host__ __device__ constexpr bool is_disc_r2(int R, int v) {
+    for (int a = 0; a <= R; ++a)
+        for (int b = 0; b <= R; ++b)
+            if (a * a + b * b == v) return true;
+    return false;
+}
+__host__ __device__ constexpr int disc_r2_rank(int R, int v) {  // distinct disc values below v
+    int n = 0;
+    for (int u = 0; u < v && u <= R * R; ++u) n += is_disc_r2(R, u) ? 1 : 0;
+    return n;
+}
+__host__ __device__ constexpr int disc_r2_count(int R) { return disc_r2_rank(R, R * R + 1); }
+
 }  // namespace vip
 
 // Record the first error of a call; launch errors come back through

@@ -24,6 +24,10 @@ constexpr int kWsStride = kMaxRadius + 1; // spatial weights stored as ws[|ky|][
 constexpr int kP = 8;                     // outputs per thread
 constexpr int kTW = 16 * kP;              // tile width in pixels
 constexpr int kLdsBudget = 160 * 1024;
+#ifndef VIP_JBF_FOLD_MAX_R  // joint kernel: folded per-r^2 colour x space tables up to this radius
+#define VIP_JBF_FOLD_MAX_R 0
+#endif
+constexpr int kFoldMaxR = VIP_JBF_FOLD_MAX_R;
 
 struct StencilArgs {
     const uint8_t* src;
@@ -40,6 +44,7 @@ struct StencilArgs {
     int dst_aligned;       // dst base and pitch are 8-byte aligned -> qword stores
     const float* color;    // colour LUT in device memory
     int lut_nonzero;       // entries [lut_nonzero, end) of the colour LUT are exactly 0
+    const float* fold;     // or null: [disc_r2_count(R)][32] = RN(ws(r^2) * colour[d]), d < 32
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 
@@ -315,8 +320,10 @@ __device__ __forceinline__ void set_progress_priority(int band) {
 // VIP_PIPE_DEPTH neighbour columns ahead: while column j's weights are
 // accumulated, the colour-LUT reads of columns j+1..j+D are already in flight
 // (the LDS latency is hidden inside the wave, not only across waves).
-// `widx(g, n01, n21, i)` returns the LDS byte address of the colour weight of
-// guide word g (source floats {b, g}, {r, 1}) for output i. Accumulation order per output is
+// `widx(g, n01, n21, i, kx)` returns the LDS byte address of the colour weight of
+// guide word g (source floats {b, g}, {r, 1}) for output i at tap column kx. FOLD: the
+// word read is already the tap's full weight ws[ky,kx] * wc[d] (a per-r^2 table, see
+// bilateral_kernel), so the spatial multiply is skipped. Accumulation order per output is
 // ascending kx, as in the reference's row-major loop.
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -337,7 +344,7 @@ __device__ __forceinline__ void fence_accumulators(f2 (&a01)[P], f2 (&a2k)[P]) {
 #ifndef VIP_ROW_LOOKAHEAD
 #define VIP_ROW_LOOKAHEAD 4  // columns between a chunk's LDS read and its first use
 #endif
-template <int HW, int L, int C0, int NC, bool FMA, bool PK, int P, bool TWO, class WIdx>
+template <int HW, int L, int C0, int NC, bool FMA, bool PK, int P, bool TWO, class WIdx, bool FOLD = false>
 __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t* splane, int row_off,
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
                                          f2 (&a01)[P], f2 (&a2k)[P]) {
@@ -366,7 +373,7 @@ __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t*
         for (int i = 0; i < P; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b], n21[b], i));
+            wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b], n21[b], i, kx));
         }
     };
 #pragma unroll
@@ -380,7 +387,7 @@ __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t*
         for (int i = 0; i < P; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            const float w = wc[b][i] * wsv[kx < 0 ? -kx : kx];
+            const float w = FOLD ? wc[b][i] : wc[b][i] * wsv[kx < 0 ? -kx : kx];
             if constexpr (FMA && PK) {
                 // v_pk_fma_f32: {s0,s1} += {b,g}*w and {s2,sk} += {r,1}*w; each half is an
                 // IEEE fma, and fma(1, w, sk) == sk + w exactly

@@ -256,17 +256,23 @@ namespace vip {
 // tests/test_oracle.py::test_constant_division_is_exact), rtv divide in double
 // (CUDA profile).
 // ---------------------------------------------------------------------------
-#ifndef VIP_GF_TW
-#define VIP_GF_TW 64
+// Guide tile (TW x TH outputs) and workgroup size, per radius. The phases run one
+// work item per thread where the counts allow it: 4 vertically adjacent blur
+// positions per pass-2 run, 4 vertically adjacent guide outputs per guide run, so a
+// (TW + 2R) x (TH + 2R) blur region of 1024 pass-2 runs fills 1024 threads once.
+// 124 x 28 at R = 2 (k = 5, C4): 128 x 32 blur positions = 1024 pass-2 runs, 868
+// guide runs, 79 KiB of LDS -> two 16-wave workgroups per CU, 60 VGPRs. Measured per
+// 4K iteration (guide stage + JBF, profiles/r02_variants.txt): 64 x 16 / 256 threads
+// 158.4-159.7 us, 124 x 28 / 1024 150.3-150.7 us (60 x 60: 157.5, 28 x 124: 154.2,
+// 252 x 12: 177.0, 60 x 28 / 512: 165.3). VIP_GF_TW / _TH / _NT override R <= 2.
+struct GfTile { int tw, th, nt; };
+constexpr GfTile gf_tile(int R) {
+#if defined(VIP_GF_TW) && defined(VIP_GF_TH) && defined(VIP_GF_NT)
+    return R <= 2 ? GfTile{VIP_GF_TW, VIP_GF_TH, VIP_GF_NT} : GfTile{64, 16, 256};
+#else
+    return R <= 2 ? GfTile{124, 28, 1024} : GfTile{64, 16, 256};
 #endif
-#ifndef VIP_GF_TH
-#define VIP_GF_TH 16
-#endif
-#ifndef VIP_GF_NT
-#define VIP_GF_NT 256
-#endif
-constexpr int kGfTW = VIP_GF_TW, kGfTH = VIP_GF_TH, kGfNT = VIP_GF_NT;
-static_assert(kGfTW % 4 == 0 && kGfTH % 4 == 0, "guide tile: 4-pixel groups, 4-row runs");
+}
 constexpr int kGfH1 = 8;   // pass 1: horizontally adjacent window aggregates per thread
 constexpr int kGfV2 = 4;   // pass 2: vertically adjacent blur positions per thread
 constexpr int kGfRun = 4;  // guide: vertically adjacent outputs per thread
@@ -275,9 +281,11 @@ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
 template <int R>
 struct GfGeom {
+    static constexpr int TW = gf_tile(R).tw, TH = gf_tile(R).th, NT = gf_tile(R).nt;
+    static_assert(TW % 4 == 0 && TH % 4 == 0, "guide tile: 4-pixel groups, 4-row runs");
     static constexpr int K = 2 * R + 1;
-    static constexpr int BW = kGfTW + 2 * R;            // BR/RR: T (+) R
-    static constexpr int BH = kGfTH + 2 * R;
+    static constexpr int BW = TW + 2 * R;               // BR/RR: T (+) R
+    static constexpr int BH = TH + 2 * R;
     static constexpr int BHP = round_up(BH, kGfV2);     // + pass-2 overhang rows
     static constexpr int HWP = round_up(BW, kGfH1);     // H: blur columns, rows of T (+) 2R
     static constexpr int HH = BHP + 2 * R;
@@ -291,12 +299,12 @@ struct GfGeom {
     static constexpr int BPL = BW * BHP;                // one BR/RR plane
     // XR, then MR in its place (gradients wait in registers until XR is consumed);
     // H after it (RB, MX words + G as u16); BR/RR and the guide tile GT reuse it all
-    static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL + kGfTW * kGfTH);
+    static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL + TW * TH);
     static constexpr int WORDS = A_WORDS;
     static_assert(MW * MH <= XR_WORDS, "MR reuses the XR region");
     static constexpr int NR1 = HH * (HWP / kGfH1);      // pass-1 runs
     static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
-    static constexpr int IT2 = (NR2 + kGfNT - 1) / kGfNT;
+    static constexpr int IT2 = (NR2 + NT - 1) / NT;
 };
 
 typedef short gf_s16x2 __attribute__((ext_vector_type(2)));
@@ -333,7 +341,7 @@ __device__ __forceinline__ void win_op(const T (&x)[N + K - 1], T (&o)[N], Op op
 // [0, height) -- and guide rows [gy0, gy1) are produced (a row slab of a sharded
 // frame; the whole frame is lo = gy0 = 0, hi = gy1 = height).
 template <int R, bool CPP>
-__global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
+__global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
                                                                    uint8_t* __restrict__ guide, int width, int lo,
                                                                    int hi, int gy0, int gy1, int ksize,
                                                                    int aligned) {
@@ -348,7 +356,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
     float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
-    const int x0 = blockIdx.x * kGfTW, y0 = gy0 + blockIdx.y * kGfTH;
+    const int x0 = blockIdx.x * G::TW, y0 = gy0 + blockIdx.y * G::TH;
     const int tid = threadIdx.x;
     // region origins (image coordinates)
     const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
@@ -360,12 +368,12 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //    (one HBM latency per tile, not one per group)
     {
         constexpr int NG = G::XH * (G::XW / 4);
-        constexpr int KG = (NG + kGfNT - 1) / kGfNT;
+        constexpr int KG = (NG + G::NT - 1) / G::NT;
         uint32_t raw[KG][3];
 #pragma unroll
         for (int k = 0; k < KG; ++k) {
-            const int g = tid + k * kGfNT;
-            if (NG % kGfNT != 0 && g >= NG) continue;
+            const int g = tid + k * G::NT;
+            if (NG % G::NT != 0 && g >= NG) continue;
             const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
             const uint8_t* row = img + (long long)clampi(yr0 + ry, H0, H1) * width * 3;
             const int x = xr0 + 4 * gx;
@@ -384,8 +392,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
         }
 #pragma unroll
         for (int k = 0; k < KG; ++k) {
-            const int g = tid + k * kGfNT;
-            if (NG % kGfNT != 0 && g >= NG) continue;
+            const int g = tid + k * G::NT;
+            if (NG % G::NT != 0 && g >= NG) continue;
             const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
             *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = unpack_rgb4(raw[k][0], raw[k][1], raw[k][2]);
         }
@@ -396,12 +404,12 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //     read directly (XR[c +- e] == X(clamp(c +- e))). sum_c h^2 + v^2 is an exact
     //     integer (< 2^24), equal to the reference's float sums: v_dot2 on the
     //     {c0, c2} 16-bit difference pairs, a mad for c1.
-    constexpr int NM = G::MW * G::MH, KM = (NM + kGfNT - 1) / kGfNT;
+    constexpr int NM = G::MW * G::MH, KM = (NM + G::NT - 1) / G::NT;
     float mrv[KM];  // this thread's gradients, stored to MR (over XR) after pass 1
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
-        const int i = tid + k * kGfNT;
-        if (NM % kGfNT != 0 && i >= NM) continue;
+        const int i = tid + k * G::NT;
+        if (NM % G::NT != 0 && i >= NM) continue;
         const int qy = i / G::MW, qx = i - qy * G::MW;
         const int cx = clampi(mr0x + qx, 0, W1) - xr0, cy = clampi(mr0y + qy, H0, H1) - yr0;
         const uint32_t* c = XR + cy * G::XW + cx;
@@ -417,7 +425,7 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     // 2b. pass 1: H = horizontal K-window aggregates, kGfH1 adjacent columns per thread.
     //     H row h <-> image row y0 - 2R + h (XR row h + 1); H column c <-> image column
     //     x0 - R + c, window XR columns c + XL - 2R .. c + XL.
-    for (int run = tid; run < G::NR1; run += kGfNT) {
+    for (int run = tid; run < G::NR1; run += G::NT) {
         const int hr = run / (G::HWP / kGfH1), hc0 = (run - hr * (G::HWP / kGfH1)) * kGfH1;
         const uint32_t* xrow = XR + (hr + 1) * G::XW + hc0 + G::XL - 2 * R;
         constexpr int NX = kGfH1 + K - 1;
@@ -447,8 +455,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     __syncthreads();  // XR is consumed (gradients and pass 1): MR takes its place
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
-        const int i = tid + k * kGfNT;
-        if (NM % kGfNT != 0 && i >= NM) continue;
+        const int i = tid + k * G::NT;
+        if (NM % G::NT != 0 && i >= NM) continue;
         MR[i] = mrv[k];
     }
     __syncthreads();
@@ -464,8 +472,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     float res[G::IT2][kGfV2][4];
 #pragma unroll
     for (int it = 0; it < G::IT2; ++it) {
-        const int run = tid + it * kGfNT;
-        if (G::NR2 % kGfNT != 0 && run >= G::NR2) continue;
+        const int run = tid + it * G::NT;
+        if (G::NR2 % G::NT != 0 && run >= G::NR2) continue;
         const int c = run % G::BW, p0 = (run / G::BW) * kGfV2;
         const int ix = x0 - R + c, iy0 = y0 - R + p0;
         uint32_t s0[kGfV2], s1[kGfV2], s2[kGfV2], smx[kGfV2];
@@ -566,8 +574,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     __syncthreads();  // H and XR are consumed: BR/RR may overwrite them
 #pragma unroll
     for (int it = 0; it < G::IT2; ++it) {
-        const int run = tid + it * kGfNT;
-        if (G::NR2 % kGfNT != 0 && run >= G::NR2) continue;
+        const int run = tid + it * G::NT;
+        if (G::NR2 % G::NT != 0 && run >= G::NR2) continue;
         const int c = run % G::BW, p0 = (run / G::BW) * kGfV2;
 #pragma unroll
         for (int j = 0; j < kGfV2; ++j) {
@@ -587,8 +595,8 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
     //    gives the row-major first argmin. Alpha blend per output.
     const float sigma_alpha = 1.f / (float)(5 * ksize);
     uint32_t* GT = lds + 4 * G::BPL;  // guide tile as RGBX words, after BR/RR
-    for (int run = tid; run < (kGfTH / kGfRun) * kGfTW; run += kGfNT) {
-        const int tx = run % kGfTW, ty0 = (run / kGfTW) * kGfRun;
+    for (int run = tid; run < (G::TH / kGfRun) * G::TW; run += G::NT) {
+        const int tx = run % G::TW, ty0 = (run / G::TW) * kGfRun;
         const int x = x0 + tx;
         if (x > W1 || y0 + ty0 >= gy1) continue;
         float rv[kGfRun + 2 * R];
@@ -633,18 +641,18 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
                 const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
                 gw |= (uint32_t)clampi((int)v, 0, 255) << (8 * c);
             }
-            GT[(ty0 + j) * kGfTW + tx] = gw;
+            GT[(ty0 + j) * G::TW + tx] = gw;
         }
     }
     __syncthreads();
 
     // 5. guide tile -> HBM: 4 RGBX words -> 3 dwords per thread (byte stores at a
     //    ragged right edge or an unaligned buffer)
-    for (int q = tid; q < kGfTH * (kGfTW / 4); q += kGfNT) {
-        const int gr = q / (kGfTW / 4), x = x0 + 4 * (q - gr * (kGfTW / 4));
+    for (int q = tid; q < G::TH * (G::TW / 4); q += G::NT) {
+        const int gr = q / (G::TW / 4), x = x0 + 4 * (q - gr * (G::TW / 4));
         const int y = y0 + gr;
         if (y >= gy1 || x > W1) continue;
-        const uint4 w = *reinterpret_cast<const uint4*>(GT + gr * kGfTW + (x - x0));
+        const uint4 w = *reinterpret_cast<const uint4*>(GT + gr * G::TW + (x - x0));
         uint8_t* row = guide + ((long long)y * width + x) * 3;
         if ((aligned & 2) && x + 3 <= W1) {
             uint32_t* d = reinterpret_cast<uint32_t*>(row);
@@ -667,14 +675,15 @@ __global__ __launch_bounds__(kGfNT) void texture_guide_fused_kernel(const uint8_
 template <int R, bool CPP>
 static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1, int ksize,
                      int aligned, hipStream_t stream) {
-    constexpr int LDS = 4 * GfGeom<R>::WORDS;
+    using G = GfGeom<R>;
+    constexpr int LDS = 4 * G::WORDS;
     static_assert(LDS <= kLdsBudget, "fused guide tile does not fit LDS");
     auto kern = texture_guide_fused_kernel<R, CPP>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     if (gy1 <= gy0) return 0;
-    dim3 grid((width + kGfTW - 1) / kGfTW, (gy1 - gy0 + kGfTH - 1) / kGfTH);
-    hipLaunchKernelGGL(kern, grid, dim3(kGfNT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
+    dim3 grid((width + G::TW - 1) / G::TW, (gy1 - gy0 + G::TH - 1) / G::TH);
+    hipLaunchKernelGGL(kern, grid, dim3(G::NT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
     return (int)hipGetLastError();
 }
 
