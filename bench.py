@@ -143,14 +143,14 @@ def cpu_baseline(cfg) -> dict:
     elif cfg["kind"] == "texture":
         # every pixel costs the same (no data-dependent work), so independent row bands
         # (each filtered as its own frame) time the same work per pixel
-        rows = 4 * threads
+        rows = cfg["rows_per_rank"]  # the whole 4K frame, one row band per thread
         img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
         parts = np.array_split(np.arange(rows), threads)
         desc = f"{w}x{rows} band split in {threads} row bands, texture ksize={k} nitr={cfg['nitr']}"
         fn = lambda: o.bands(lambda a, b: o.texture(img[a:b], k, cfg["nitr"], profile=o.CPP),  # noqa: E731
                              [(int(p[0]), int(p[-1]) + 1) for p in parts], threads)
     else:
-        rows = {7: 2160, 15: 64}.get(k // 2, 256)
+        rows = {7: 2160, 15: 256}.get(k // 2, 256)
         img = o.random_u8(w * rows * 3).reshape(rows, w, 3)
         f = o.adaptive if cfg["kind"] == "adaptive" else o.bilateral
         desc = f"{w}x{rows} {'frame' if rows == 2160 else 'band'}, {cfg['kind']} ksize={k}"
@@ -215,6 +215,53 @@ def valu_issue(config: str, kernel: str, launch_ms: float):
     return out
 
 
+def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms) -> dict:
+    """C4: the dominant kernel of the iteration (the larger of the fused guide stage and
+    the joint bilateral, live event-timed per launch) with its own roof, the other one
+    beside it, and the pipeline's HBM rate from the bytes the kernels actually move
+    (committed PMC summary, per frame) -- not the unfused stage-wise decomposition."""
+    nitr, k = cfg["nitr"], cfg["ksize"]
+    rj = k - 1                                   # JBF radius: ksize 2k - 1
+    taps = circle_taps(rj)
+    guide_k, jbf_k = "void vip::texture_guide_fused_kernel", f"void vip::bilateral_kernel<{rj},"
+    out = {}
+    if stage_ms:
+        g_ms, j_ms = stage_ms["guide"], stage_ms["jbf"]
+        jbf_tf = 8.0 * taps * px / (j_ms * 1e-3) / 1e12
+        jbf = dict(kernel=f"joint bilateral_kernel<R={rj}> (ksize {2 * k - 1}, {taps} taps)", avg_launch_ms=round(j_ms, 4),
+                   bound="valu-fp32", achieved=round(jbf_tf, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
+                   frac=round(jbf_tf / PEAK_FP32_TFLOPS, 4), flop_per_px=8 * taps,
+                   valu_issue=valu_issue(config, jbf_k, j_ms))
+        g_gbs = 6.0 * px / (g_ms * 1e-3) / 1e9  # reads the frame, writes the guide
+        gtraffic, gsrc = pmc_traffic(config, [guide_k])
+        guide = dict(kernel="texture_guide_fused_kernel (gradient + blur/mRTV + argmin/alpha guide, fused)",
+                     avg_launch_ms=round(g_ms, 4), bound="valu-issue", bytes_per_px=6,
+                     hbm=dict(achieved=round(g_gbs, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(g_gbs / PEAK_HBM_GBS, 4),
+                              traffic=gtraffic, traffic_source=gsrc),
+                     valu_issue=valu_issue(config, guide_k, g_ms))
+        dom, other = (jbf, guide) if j_ms >= g_ms else (guide, jbf)
+        if dom is jbf:
+            jtraffic, jsrc = pmc_traffic(config, [jbf_k])
+            out.update(bound="valu-fp32", achieved=jbf["achieved"], peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
+                       frac=jbf["frac"], traffic=jtraffic, traffic_source=jsrc, traffic_algorithmic=9.0 * px)
+        else:
+            out.update(bound="hbm", achieved=guide["hbm"]["achieved"], peak=PEAK_HBM_GBS, unit="GB/s",
+                       frac=guide["hbm"]["frac"], traffic=guide["hbm"]["traffic"], traffic_source=guide["hbm"]["traffic_source"],
+                       traffic_algorithmic=6.0 * px)
+        out.update(kernel=dom["kernel"], avg_launch_ms=dom["avg_launch_ms"], dominant=dom, other=other,
+                   stage_split=dict(method="timed-region frame time split by the guide:JBF ratio of evented frames",
+                                    guide_evented_ms=round(stage_ms["guide_evented"], 4),
+                                    jbf_evented_ms=round(stage_ms["jbf_evented"], 4)))
+    traffic, tsrc = pmc_traffic(config, [guide_k, jbf_k], nitr)
+    pipe = dict(frame_ms=round(frame_ms, 4), launches=2 * nitr, traffic_per_frame=traffic, traffic_source=tsrc)
+    if traffic:
+        gbs = traffic / (frame_ms * 1e-3) / 1e9
+        pipe.update(hbm_achieved=round(gbs, 2), hbm_peak=PEAK_HBM_GBS, hbm_frac=round(gbs / PEAK_HBM_GBS, 4),
+                    fused_floor_bytes=6.0 * px * nitr)
+    out["pipeline"] = pipe
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -267,9 +314,16 @@ def main():
         tex = _TextureImpl(w, rows, k, cfg["nitr"])
         srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
+        smarks = []
 
         def run(i):
             tex.execute(srcs[i % NBUF], dsts[i % NBUF], stream=stream)
+
+        def run_staged(i):
+            """one frame with per-stage events (vip_texture_run_timed)"""
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * cfg["nitr"] + 1)]
+            tex.execute_timed(srcs[i % NBUF], dsts[i % NBUF], ev, stream=stream)
+            smarks.append(ev)
     elif cfg["kind"] == "texture":
         # row-sharded frame: one halo exchange of nitr * texture_halo_rows(k) rows per
         # frame, then shrinking ghost zones (sharded.ShardedTexture)
@@ -342,6 +396,22 @@ def main():
         kernel_ms = sum(m[1].elapsed_time(m[2]) for m in marks[:n]) / n
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    stage_ms = None
+    if cfg["kind"] == "texture" and world == 1:
+        # Per-stage split of the frame: an event between two launches costs a few us of
+        # stream time (measured: +4 us on each stage against rocprofv3), so the timed
+        # frames above carry no inner events; max(4, K/4) further frames, after the
+        # timed region, record events around every launch, and their guide : JBF ratio
+        # splits the clean frame time of the timed region (stage_ms, per launch).
+        for i in range(max(4, args.steps // 4)):
+            run_staged(args.warmup + args.steps + i)
+        torch.cuda.synchronize(dev)
+        nit = cfg["nitr"]
+        guide = sum(m[2 * t].elapsed_time(m[2 * t + 1]) for m in smarks for t in range(nit))
+        jbf = sum(m[2 * t + 1].elapsed_time(m[2 * t + 2]) for m in smarks for t in range(nit))
+        per = kernel_ms / nit
+        stage_ms = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
+                    "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
     t = torch.tensor([elapsed, kernel_ms, exchange_ms or 0.0], dtype=torch.float64,
                      device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
@@ -355,16 +425,7 @@ def main():
     value = total_px / (elapsed / args.steps) / 1e6
 
     if cfg["kind"] == "texture":
-        # stage-wise algorithmic bytes per pixel per iteration: grad 3+4,
-        # blur_rtv 7+16, guide 16+3, JBF 6+3 = 58 B
-        bytes_launch = 58.0 * px_per_rank * cfg["nitr"]
-        achieved = bytes_launch / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = (None, None) if world > 1 else pmc_traffic(
-            args.config, ["void vip::texture_guide_fused_kernel", "void vip::bilateral_kernel"], cfg["nitr"])
-        roof = dict(bound="hbm", achieved=round(achieved, 2), peak=PEAK_HBM_GBS, unit="GB/s",
-                    frac=round(achieved / PEAK_HBM_GBS, 4), traffic=traffic, traffic_source=tsrc,
-                    kernel="whole texture pipeline per launch (gradient, blur_rtv, guide, JBF) x nitr",
-                    avg_launch_ms=round(kernel_ms, 4))
+        roof = texture_roofline(args.config, cfg, px_per_rank, kernel_ms, stage_ms)
     else:
         taps = circle_taps(r)
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank

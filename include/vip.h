@@ -116,6 +116,11 @@ int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int
 int vip_texture_destroy(vip_texture_t h);
 /* Impl::execute (:199-214); d_src and d_dst are dense width*3 */
 int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream);
+/* vip_texture_run with per-stage timestamps (measurement; no reference counterpart):
+ * `events` holds 2*nitr + 1 hipEvent_t (created with timing enabled, passed as void*);
+ * events[2i] is recorded on `stream` before iteration i's guide stage, events[2i+1]
+ * before its joint bilateral, events[2*nitr] after the last launch. */
+int vip_texture_run_timed(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream, void* const* events);
 
 /* Row-slab form of one texture iteration for a row-sharded frame (SURVEY §8(f)3;
  * the reference is single-GPU). d_src is a dense slab of the handle's width x

@@ -386,16 +386,13 @@ int vip_texture_guide(vip_texture_t h, const float* d_blurred, const float* d_rt
                         (hipStream_t)stream);
 }
 
-// Impl::execute (src/bilateral_texture_filter_impl.cu:199-214) without the
-// nitr + 2 device-to-device copies: iteration i reads X_i and writes X_{i+1},
-// X_0 = d_src, X_nitr = d_dst, intermediates alternate between two scratch frames.
-// Each iteration is two launches: the fused guide stage and the joint bilateral.
-int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream) {
+static int texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream, void* const* events) {
     if (!h || !d_src || !d_dst) return VIP_ERR_INVALID_ARGUMENT;
     const hipStream_t s = (hipStream_t)stream;
     const size_t bytes = (size_t)h->width * h->height * 3;
     const size_t pitch = (size_t)h->width * 3;
     if (h->nitr == 0) {
+        if (events) VIP_HIP_CHECK(hipEventRecord((hipEvent_t)events[0], s));
         if (d_src != d_dst) VIP_HIP_CHECK(hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, s));
         return 0;
     }
@@ -407,13 +404,29 @@ int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void*
     for (int it = 0; it < h->nitr; ++it) {
         uint8_t* next = (it == h->nitr - 1) ? d_dst : (cur == h->d_ping[0] ? h->d_ping[1] : h->d_ping[0]);
         // gradient -> blur/mRTV -> guide fused in LDS (one launch), then the JBF
+        if (events) VIP_HIP_CHECK(hipEventRecord((hipEvent_t)events[2 * it], s));
         int rc = launch_texture_guide_fused(cur, h->d_guide, h->width, h->height, h->ksize,
                                             h->numerics == VIP_NUMERICS_CPP, s);
+        if (!rc && events) rc = (int)hipEventRecord((hipEvent_t)events[2 * it + 1], s);
         if (!rc) rc = vip_joint_bilateral_run(h->jbf, cur, pitch, h->d_guide, pitch, next, pitch, stream);
         if (rc) return rc;
         cur = next;
     }
+    if (events) VIP_HIP_CHECK(hipEventRecord((hipEvent_t)events[2 * h->nitr], s));
     return 0;
+}
+
+// Impl::execute (src/bilateral_texture_filter_impl.cu:199-214) without the
+// nitr + 2 device-to-device copies: iteration i reads X_i and writes X_{i+1},
+// X_0 = d_src, X_nitr = d_dst, intermediates alternate between two scratch frames.
+// Each iteration is two launches: the fused guide stage and the joint bilateral.
+int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream) {
+    return texture_run(h, d_src, d_dst, stream, nullptr);
+}
+
+int vip_texture_run_timed(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream, void* const* events) {
+    if (!events) return VIP_ERR_INVALID_ARGUMENT;
+    return texture_run(h, d_src, d_dst, stream, events);
 }
 
 int vip_texture_halo_rows(int ksize) {

@@ -181,6 +181,19 @@ class _TextureImpl(_Handle):
         n = self.width * self.height * 3
         call("vip_texture_run", self._h, _ptr(d_src, n), _ptr(d_dst, n), _stream(stream))
 
+    def execute_timed(self, d_src, d_dst, events, stream=None):
+        """execute() with per-stage timestamps (include/vip.h vip_texture_run_timed):
+        `events` = 2 * nitr + 1 torch.cuda.Event(enable_timing=True), recorded before
+        each iteration's guide stage, before its joint bilateral, and after the last."""
+        n = self.width * self.height * 3
+        if len(events) != 2 * self.nitr + 1:
+            raise ValueError(f"need {2 * self.nitr + 1} events, got {len(events)}")
+        for e in events:  # torch creates the HIP event lazily, at its first record
+            if not e.cuda_event:
+                e.record(stream) if stream is not None and not isinstance(stream, int) else e.record()
+        arr = (ctypes.c_void_p * len(events))(*[e.cuda_event for e in events])
+        call("vip_texture_run_timed", self._h, _ptr(d_src, n), _ptr(d_dst, n), _stream(stream), arr)
+
     def compute_blur_and_rtv(self, d_image, d_magnitude, d_blurred, d_rtv, stream=None):
         n = self.width * self.height
         call("vip_texture_blur_rtv", self._h, _ptr(d_image, 3 * n), _ptr(d_magnitude, 4 * n, "float32"),
