@@ -70,11 +70,20 @@ CONFIGS = {
 FLOP_PER_TAP = {"bilateral": 8, "adaptive": 13}
 
 
+DEFAULT_STEPS = {"c1": 2000, "c2": 2000, "c3": 1000, "c4": 500, "c5": 20}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    # defaults: a timed region of ~0.3-0.5 s per config (DEFAULT_STEPS), after a clock
+    # settle period and W warm-up steps
+    p.add_argument("--steps", type=int, default=None)
+    p.add_argument("--warmup", type=int, default=20)
+    # MI355X clocks ramp over ~1 s of sustained load (measured, C2 r=7 4K: 0.219 ms per
+    # frame after 3 warm-up steps, 0.179 ms after 200): keep launching untimed steps for
+    # this long before the W warm-up steps so the timed steps see the steady clock
+    p.add_argument("--settle-s", type=float, default=1.0)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     # rehearsal only: gloo + every rank on cuda:0 runs the N>1 code path on a 1-GPU box
@@ -268,6 +277,8 @@ def main():
     import torch.distributed as dist
 
     cfg = CONFIGS[args.config]
+    if args.steps is None:
+        args.steps = DEFAULT_STEPS[args.config]
     if "data" in cfg and args.data == "uniform":
         args.data = cfg["data"]
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -353,7 +364,7 @@ def main():
     # after them (an event pair costs ~11 us of stream time, measured with rocprofv3,
     # so not every step carries them): exchange_ms and kernel_ms per rank.
     KSAMPLE = 4
-    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range((args.steps + KSAMPLE - 1) // KSAMPLE)]
     timed = {"on": False, "i": 0, "n": 0}
 
     def step(i):
@@ -371,6 +382,15 @@ def main():
         if timed["on"]:
             timed["i"] += 1
 
+    # clock settle (untimed): steps for --settle-s seconds of wall time, checked every
+    # few steps with a device sync; then the W warm-up steps
+    t_settle, i_settle = time.perf_counter(), 0
+    while time.perf_counter() - t_settle < args.settle_s:
+        for _ in range(8):
+            run(i_settle)
+            i_settle += 1
+        torch.cuda.synchronize(dev)
+    settle_steps = i_settle
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize(dev)
@@ -465,6 +485,7 @@ def main():
         # per step, max over ranks: the kernel(s) and, at N>1, the halo exchange before
         # them (event-timed on the filter stream every 4th step)
         "kernel_ms": round(kernel_ms, 4),
+        "settle": {"seconds": args.settle_s, "steps": settle_steps},
         **({"exchange_ms": round(exchange_ms, 4)} if exchange_ms is not None else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

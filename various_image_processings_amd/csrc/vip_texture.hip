@@ -336,6 +336,20 @@ __device__ __forceinline__ void win_op(const T (&x)[N + K - 1], T (&o)[N], Op op
     for (int j = 0; j < N; ++j) o[j] = (j % K == 0) ? suf[j] : op(suf[j], pre[j + K - 1]);
 }
 
+#ifdef VIP_GF_STAMPS
+// diagnostic build only: [workgroup][wave][8] shader-clock stamps -- kernel entry, the
+// arrival of each wave at each of the 6 phase barriers, exit
+__device__ unsigned long long vip_gf_stamps[4096 * 16 * 8];
+#define VIP_GF_STAMP(k)                                                                             \
+    do {                                                                                            \
+        const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                         \
+        if ((threadIdx.x & 63) == 0 && wg_ < 4096)                                                  \
+            vip_gf_stamps[(wg_ * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define VIP_GF_STAMP(k)
+#endif
+
 // Row bands: rows [lo, hi) of the (dense, width*3 pitch) buffers are the valid
 // frame rows -- every stage clamps into them, as the reference clamps into
 // [0, height) -- and guide rows [gy0, gy1) are produced (a row slab of a sharded
@@ -357,6 +371,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
     float* RR = BR + 3 * G::BPL;
     float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
     const int x0 = blockIdx.x * G::TW, y0 = gy0 + blockIdx.y * G::TH;
+    VIP_GF_STAMP(0);
     const int tid = threadIdx.x;
     // region origins (image coordinates)
     const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
@@ -377,6 +392,13 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
             const uint8_t* row = img + (long long)clampi(yr0 + ry, H0, H1) * width * 3;
             const int x = xr0 + 4 * gx;
+#ifdef VIP_GF_ABL_LOAD  // timing ablation only (wrong output): no HBM reads
+            if (true) {
+                raw[k][0] = g * 0x01010101u;
+                raw[k][1] = (g + x) * 0x01010101u;
+                raw[k][2] = (g ^ 7) * 0x01010101u;
+            } else
+#endif
             if ((aligned & 1) && x >= 0 && x + 3 <= W1) {
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
                 raw[k][0] = w[0];
@@ -398,6 +420,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = unpack_rgb4(raw[k][0], raw[k][1], raw[k][2]);
         }
     }
+    VIP_GF_STAMP(1);
     __syncthreads();
 
     // 2a. MR[q] = gradient at c = clamp(q); XR is pre-clamped, so c's neighbours are
@@ -452,6 +475,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             *reinterpret_cast<uint4*>(h + G::HPL + j) = make_uint4(omx[j], omx[j + 1], omx[j + 2], omx[j + 3]);
         }
     }
+    VIP_GF_STAMP(2);
     __syncthreads();  // XR is consumed (gradients and pass 1): MR takes its place
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -459,6 +483,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
         if (NM % G::NT != 0 && i >= NM) continue;
         MR[i] = mrv[k];
     }
+    VIP_GF_STAMP(3);
     __syncthreads();
 
     // 3. pass 2: blur + mRTV at the BR positions, kGfV2 vertically adjacent positions per
@@ -568,9 +593,14 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             const float imax = div_exact(smx[j] & 0xffffu, 3.f, kThird);
             const float imin = div_exact(1023u - (smx[j] >> 16), 3.f, kThird);
             const float num = (imax - imin) * mmax[j];
+#ifdef VIP_GF_ABL_DIV  // timing ablation only (inexact): f32 divide instead of the double one
+            res[it][j][3] = num / (msum[j] + 1e-9f);
+#else
             res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+#endif
         }
     }
+    VIP_GF_STAMP(4);
     __syncthreads();  // H and XR are consumed: BR/RR may overwrite them
 #pragma unroll
     for (int it = 0; it < G::IT2; ++it) {
@@ -586,6 +616,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             RR[i] = res[it][j][3];
         }
     }
+    VIP_GF_STAMP(5);
     __syncthreads();
 
     // 4. guide: first strict argmin of rtv over the window (RR is pre-clamped, so the
@@ -631,7 +662,11 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             }
             const int ci = (ty0 + j + R) * G::BW + tx + R;
             const float arg = sigma_alpha * (RR[ci] - rmin);
+#ifdef VIP_GF_ABL_EXP  // timing ablation only (inexact): hardware exp2
+            const float e = __builtin_amdgcn_exp2f(arg * 1.44269504f);
+#else
             const float e = (float)exp((double)arg);
+#endif
             const float alpha = 2.f / (1.f + e) - 1.f;
             const float beta = 1.f - alpha;
             uint32_t gw = 0;
@@ -644,6 +679,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             GT[(ty0 + j) * G::TW + tx] = gw;
         }
     }
+    VIP_GF_STAMP(6);
     __syncthreads();
 
     // 5. guide tile -> HBM: 4 RGBX words -> 3 dwords per thread (byte stores at a
@@ -670,6 +706,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
             }
         }
     }
+    VIP_GF_STAMP(7);
 }
 
 template <int R, bool CPP>
@@ -718,3 +755,9 @@ int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, in
 }
 
 }  // namespace vip
+
+#ifdef VIP_GF_STAMPS
+extern "C" int vip_debug_read_gf_stamps(void* host, size_t bytes) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(vip::vip_gf_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#endif
