@@ -25,11 +25,11 @@ f = _TextureImpl(W, H, 5, 1)
 for _ in range(3):
     f.execute(src, dst)
 torch.cuda.synchronize()
-buf = np.zeros(4096 * 16 * 8, np.uint64)
+buf = np.zeros(4096 * 16 * 16, np.uint64)
 lib = L.lib()
 lib.vip_debug_read_gf_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 assert lib.vip_debug_read_gf_stamps(buf.ctypes.data, buf.nbytes) == 0
-s = buf.reshape(4096, 16, 8).astype(np.int64)
+s = buf.reshape(4096, 16, 16).astype(np.int64)
 valid = (s[:, 0, 0] > 0) & (s[:, 0, 7] > s[:, 0, 0])
 s = s[valid]
 names = ["xr load", "gradient+pass1", "MR store", "pass2", "BR/RR store", "guide", "store"]
@@ -45,6 +45,12 @@ for k in range(1, 8):
                          "share": round(float(length / tot), 3)}
     prev = arr.max(axis=1)
 res["tile_lifetime_cycles"] = round(float(tot))
+# inside phases, per wave: XR loads issued (8) and gradients done (9)
+res["xr issue (entry -> loads issued)"] = round(float((s[:, :, 8] - start[:, None]).mean()))
+res["xr wait+unpack (issued -> barrier arrival)"] = round(float((s[:, :, 1] - s[:, :, 8]).mean()))
+b1 = s[:, :, 1].max(axis=1)
+res["gradients (barrier 1 -> done)"] = round(float((s[:, :, 9] - b1[:, None]).mean()))
+res["pass 1 (gradients done -> barrier 2 arrival)"] = round(float((s[:, :, 2] - s[:, :, 9]).mean()))
 # concurrency: how many workgroups overlap in time per CU is not visible here; the
 # span of all stamps gives the kernel's clock count
 res["kernel_span_cycles"] = int(s[:, :, 7].max() - s[:, :, 0].min())

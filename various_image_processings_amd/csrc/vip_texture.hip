@@ -337,14 +337,15 @@ __device__ __forceinline__ void win_op(const T (&x)[N + K - 1], T (&o)[N], Op op
 }
 
 #ifdef VIP_GF_STAMPS
-// diagnostic build only: [workgroup][wave][8] shader-clock stamps -- kernel entry, the
-// arrival of each wave at each of the 6 phase barriers, exit
-__device__ unsigned long long vip_gf_stamps[4096 * 16 * 8];
+// diagnostic build only: [workgroup][wave][16] shader-clock stamps -- kernel entry (0),
+// the arrival of each wave at each of the 6 phase barriers (1-6), exit (7), XR loads
+// issued (8), gradients done (9)
+__device__ unsigned long long vip_gf_stamps[4096 * 16 * 16];
 #define VIP_GF_STAMP(k)                                                                             \
     do {                                                                                            \
         const int wg_ = blockIdx.y * gridDim.x + blockIdx.x;                                         \
         if ((threadIdx.x & 63) == 0 && wg_ < 4096)                                                  \
-            vip_gf_stamps[(wg_ * 16 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+            vip_gf_stamps[(wg_ * 16 + (threadIdx.x >> 6)) * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
 #else
 #define VIP_GF_STAMP(k)
@@ -412,6 +413,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
                 raw[k][2] = (q2 >> 16) | (q3 << 8);
             }
         }
+VIP_GF_STAMP(8);
 #pragma unroll
         for (int k = 0; k < KG; ++k) {
             const int g = tid + k * G::NT;
@@ -445,6 +447,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
                                               false);
         mrv[k] = __builtin_sqrtf((float)ss);
     }
+    VIP_GF_STAMP(9);
     // 2b. pass 1: H = horizontal K-window aggregates, kGfH1 adjacent columns per thread.
     //     H row h <-> image row y0 - 2R + h (XR row h + 1); H column c <-> image column
     //     x0 - R + c, window XR columns c + XL - 2R .. c + XL.
