@@ -31,11 +31,15 @@ if "--r15" in sys.argv:  # one 2048-row slab of the C5 frame (16384 wide, ksize 
     d15 = torch.empty((2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda")
     b31 = _BilateralImpl(16384, 2048 + 30, 31)
     cases += [("bilateral_r15_slab", lambda s, d: b31.bilateral_filter(s15[0], d15))]
+import time
 for name, f in cases:
-    for i in range(3): f(srcs[i % 6], dst)
-    torch.cuda.synchronize()
+    # clock settle: 1 s of back-to-back launches (MI355X clocks ramp under sustained load)
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 1.0:
+        for i in range(8): f(srcs[i % 6], dst)
+        torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    n = 30
+    n = 100
     e0.record()
     for i in range(n): f(srcs[i % 6], dst)
     e1.record(); torch.cuda.synchronize()

@@ -43,6 +43,9 @@ __device__ __forceinline__ void vip_rt_stamp(int k) {
 #ifndef VIP_BIL_UNROLL_MAX_R
 #define VIP_BIL_UNROLL_MAX_R 15
 #endif
+#ifndef VIP_BIL_PIPE_DEPTH  // plain bilateral: LUT reads this many neighbour columns ahead
+#define VIP_BIL_PIPE_DEPTH VIP_PIPE_DEPTH
+#endif
 #ifndef VIP_BIL_RCP  // epilogue: one exact reciprocal per output instead of 3 IEEE divides
 #define VIP_BIL_RCP 1
 #endif
@@ -152,7 +155,8 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
                         }
                         return ad;
                     };
-                    row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT, decltype(widx)&, FOLD>(
+                    row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT, decltype(widx)&, FOLD,
+                             JOINT ? VIP_PIPE_DEPTH : VIP_BIL_PIPE_DEPTH>(
                         gplane, splane, row_off, wsv, lut_bytes, widx, a01, a2k);
                     if constexpr (ROW_UNROLL) fence_accumulators(a01, a2k);
             });

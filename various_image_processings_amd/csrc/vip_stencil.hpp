@@ -344,11 +344,11 @@ __device__ __forceinline__ void fence_accumulators(f2 (&a01)[P], f2 (&a2k)[P]) {
 #ifndef VIP_ROW_LOOKAHEAD
 #define VIP_ROW_LOOKAHEAD 4  // columns between a chunk's LDS read and its first use
 #endif
-template <int HW, int L, int C0, int NC, bool FMA, bool PK, int P, bool TWO, class WIdx, bool FOLD = false>
+template <int HW, int L, int C0, int NC, bool FMA, bool PK, int P, bool TWO, class WIdx, bool FOLD = false,
+          int D = VIP_PIPE_DEPTH>
 __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t* splane, int row_off,
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
                                          f2 (&a01)[P], f2 (&a2k)[P]) {
-    constexpr int D = VIP_PIPE_DEPTH;
     constexpr int NB = D + 1;            // ring of in-flight columns
     constexpr int J0 = L - HW;           // first neighbour column relative to the thread's P
     constexpr int J1 = L + P - 1 + HW;   // last
