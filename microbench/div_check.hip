@@ -7,7 +7,8 @@
 // (b) the quotient for 2^30 pseudo-random (s, k), s in [0, 255 k], and for s at the
 //     float midpoints' neighbourhoods -- Markstein's theorem makes (b) follow from (a),
 //     this is the empirical cross-check.
-// Exit status 0 iff no mismatch against the IEEE divide (hipcc default, correctly
+// (c) vip::sqrt_int_exact against sqrtf for every integer in [0, 2^20) (texture gradient).
+// Exit status 0 iff no mismatch against the IEEE divide / sqrt (hipcc default, correctly
 // rounded). Run on the GPU: tests/test_gpu_parity.py::test_epilogue_division_exact.
 #include <hip/hip_runtime.h>
 
@@ -16,7 +17,16 @@
 
 #include "vip_stencil.hpp"
 
-__device__ unsigned long long g_bad[2];
+__device__ unsigned long long g_bad[3];
+
+// (c) the texture gradient's integer square root: vip::sqrt_int_exact == sqrtf (hipcc's
+//     correctly rounded expansion) for every integer in [0, n)
+__global__ void sqrt_ints(uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = (float)i;
+    if (__float_as_uint(vip::sqrt_int_exact(x)) != __float_as_uint(__builtin_sqrtf(x))) atomicAdd(&g_bad[2], 1ull);
+}
 
 __global__ void recip_all(uint32_t lo_bits, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -52,7 +62,7 @@ __global__ void quot_random(uint64_t base) {
 }
 
 int main() {
-    unsigned long long zero[2] = {0, 0};
+    unsigned long long zero[3] = {0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero)) != hipSuccess) return 2;
     const uint32_t lo = 0x3f800000u, hi = 0x44800000u;  // bit patterns of 1.0f and 1024.0f
     const uint32_t n = hi - lo;
@@ -60,9 +70,12 @@ int main() {
     const uint64_t per = 1ull << 26;
     for (int rep = 0; rep < 16; ++rep)
         hipLaunchKernelGGL(quot_random, dim3((unsigned)(per / 256)), dim3(256), 0, 0, rep * per);
-    unsigned long long bad[2];
+    const uint32_t nsq = 1u << 20;
+    hipLaunchKernelGGL(sqrt_ints, dim3(nsq / 256), dim3(256), 0, 0, nsq);
+    unsigned long long bad[3];
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
     std::printf("reciprocal: %u floats k in [1, 1024), %llu mismatches\n", n, bad[0]);
     std::printf("quotient: %llu random (s, k), %llu mismatches\n", (unsigned long long)(16 * per), bad[1]);
-    return (bad[0] || bad[1]) ? 1 : 0;
+    std::printf("integer sqrt: %u integers in [0, 2^20), %llu mismatches\n", nsq, bad[2]);
+    return (bad[0] || bad[1] || bad[2]) ? 1 : 0;
 }

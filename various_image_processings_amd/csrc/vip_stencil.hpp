@@ -412,6 +412,20 @@ __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t*
     }
 }
 
+// RN(sqrt(x)) for x = 0 or x in [1, 2^24) (the texture gradient's integer sums of
+// squares): the hardware v_sqrt_f32 result s and one neighbour check each way -- the
+// refinement LLVM's correctly rounded sqrtf expansion applies, without its denormal
+// scaling and special-value handling, which these arguments never need. 9 VALU
+// instead of 17; microbench/div_check.hip verifies it against sqrtf for EVERY integer
+// in [0, 2^20) (the gradient sums stay below 6 * 255^2 = 390150).
+__device__ __forceinline__ float sqrt_int_exact(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float s1 = __builtin_fmaf(-sm, s, x) <= 0.f ? sm : s;
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    return __builtin_fmaf(-sp, s, x) > 0.f ? sp : s1;
+}
+
 // RN(1/k) for k in [1, 1024): hardware rcp (1 ulp) + one Newton step. Verified
 // exhaustively over every float of that range by microbench/div_check.hip.
 __device__ __forceinline__ float recip_exact(float k) {

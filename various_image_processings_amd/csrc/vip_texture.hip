@@ -445,7 +445,11 @@ VIP_GF_STAMP(8);
         const int v1 = (int)__builtin_amdgcn_ubfe(D, 8, 8) - (int)__builtin_amdgcn_ubfe(U, 8, 8);
         const int ss = __builtin_amdgcn_sdot2(h02, h02, __builtin_amdgcn_sdot2(v02, v02, h1 * h1 + v1 * v1, false),
                                               false);
+#ifdef VIP_GF_LLVM_SQRT  // the compiler's correctly rounded expansion (same result, 17 VALU)
         mrv[k] = __builtin_sqrtf((float)ss);
+#else
+        mrv[k] = sqrt_int_exact((float)ss);  // == sqrtf, exhaustively checked (microbench/div_check)
+#endif
     }
     VIP_GF_STAMP(9);
     // 2b. pass 1: H = horizontal K-window aggregates, kGfH1 adjacent columns per thread.
