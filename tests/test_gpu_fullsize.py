@@ -10,6 +10,7 @@ both side borders. Bands are independent, so they run in parallel threads.
   C3 adaptive r=7 3840x2160            test_c3_adaptive_4k
   C4 texture k=5 nitr=5 3840x2160      test_c4_texture_4k (bands on crops with a 45-row ghost margin)
   C5 bilateral r=15 16384x16384        test_c5_bilateral_16k_single_launch_and_8_way_split
+  C3 / C4 frames split 8 ways          test_4k_8_way_split_equals_single_launch
 References: src/adaptive_bilateral_filter_impl.cu:7-115,
 src/bilateral_texture_filter_impl.cu:199-214, src/bilateral_filter_impl.cu:7-96.
 """
@@ -97,3 +98,34 @@ def test_c5_bilateral_16k_single_launch_and_8_way_split(dev, oracle):
         sb.filter(slab, out, exchange=False)
         torch.cuda.synchronize()
         assert torch.equal(out, d_full[b:e]), f"rank {rank}: {int((out != d_full[b:e]).sum())} bytes differ"
+
+
+@pytest.mark.parametrize("kind", ["adaptive", "texture"])
+def test_4k_8_way_split_equals_single_launch(dev, oracle, kind):
+    """SURVEY 8(f)3 at BASELINE size: the C3 / C4 frame split 8 ways (ShardedBilateral
+    adaptive with a 7-row halo; ShardedTexture with one 45-row halo per frame and
+    shrinking ghost zones) equals the single-GPU launch on every pixel. Each rank's slab
+    holds its rows plus the neighbours' halo rows a real exchange would deliver."""
+    import torch
+    from various_image_processings_amd.sharded import ShardedBilateral, ShardedTexture
+    w, h = 3840, 2160
+    img = oracle.random_image(w, h)
+    d_src = dev.put(img)
+    d_full = dev.empty(img.shape)
+    if kind == "texture":
+        vip.CudaBilateralTextureFilter(w, h, 5, 5).execute(d_src, d_full)
+    else:
+        vip.CudaAdaptiveBilateralFilter(w, h, 15).execute(d_src, d_full)
+    for rank in range(8):
+        sh = ShardedTexture(w, h, 5, 5, rank, 8) if kind == "texture" else \
+            ShardedBilateral(w, h, 15, rank, 8, adaptive=True)
+        g = sh.geo
+        b, e = g.rows
+        r = g.radius
+        slab = torch.zeros((g.slab_rows, w, 3), dtype=torch.uint8, device="cuda")
+        lo, hi = max(b - r, 0), min(e + r, h)
+        slab[r - (b - lo):r + g.own + (hi - e)] = d_src[lo:hi]
+        out = torch.empty((g.own, w, 3), dtype=torch.uint8, device="cuda")
+        sh.filter(slab, out, exchange=False)
+        torch.cuda.synchronize()
+        assert torch.equal(out, d_full[b:e]), f"{kind} rank {rank}: {int((out != d_full[b:e]).sum())} bytes differ"
