@@ -426,7 +426,7 @@ __device__ __forceinline__ float sqrt_int_exact(float x) {
     return __builtin_fmaf(-sp, s, x) > 0.f ? sp : s1;
 }
 
-// RN(1/k) for k in [1, 1024): hardware rcp (1 ulp) + one Newton step. Verified
+// RN(1/k) for k in [1, 2^17): hardware rcp (1 ulp) + one Newton step. Verified
 // exhaustively over every float of that range by microbench/div_check.hip.
 __device__ __forceinline__ float recip_exact(float k) {
     const float y0 = __builtin_amdgcn_rcpf(k);

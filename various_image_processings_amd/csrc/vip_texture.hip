@@ -674,7 +674,9 @@ VIP_GF_STAMP(8);
 #else
             const float e = (float)exp((double)arg);
 #endif
-            const float alpha = 2.f / (1.f + e) - 1.f;
+            // 2 / (1 + e) == 2 * RN(1 / (1 + e)) exactly (a power-of-two scale); e >= 1, so
+            // recip_exact's argument is in [2, 2^17) here, where div_check verifies it
+            const float alpha = 2.f * recip_exact(1.f + e) - 1.f;
             const float beta = 1.f - alpha;
             uint32_t gw = 0;
 #pragma unroll
