@@ -92,6 +92,9 @@ def parse():
     # SURVEY 8(d) inputs: (i) uniform 0..254 like test/random_array.hpp (default), (ii) narrow
     # uniform [100, 120) like sample/benchmark/main.cpp:213, (iii) lenna tiled to the frame
     p.add_argument("--data", default="uniform", choices=["uniform", "narrow", "lenna"])
+    # the reference's sample/benchmark table instead of the contract line
+    p.add_argument("--sample-table", action="store_true")
+    p.add_argument("--sample-size", default="100x100")
     return p.parse_args()
 
 
@@ -271,8 +274,57 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms)
     return out
 
 
+def sample_table(args) -> None:
+    """The reference's sample/benchmark/main.cpp:105-213 table: every filter timed on the
+    include/cpp path and on the GPU path side by side, on a randu(100, 120) image of
+    --sample-size (default 100x100), ksize 9, texture ksize 9 nitr 3
+    (sample/benchmark/config.toml), one discarded warm-up then the mean of 10 calls
+    (MEASURE, :20-33). cpp = the oracle's CPP profile (include/cpp numerics) in row bands
+    on the host cores; hip = the blocking public API on device-resident frames."""
+    import torch
+
+    import various_image_processings_amd as vip
+    from oracle import oracle as o
+    w, h = (int(v) for v in args.sample_size.split("x"))
+    threads, model = host_cores()
+    img = 100 + o.random_u8(w * h * 3, 20).reshape(h, w, 3)
+    d_src = torch.from_numpy(img).cuda()
+    d_dst, d_mag = torch.empty_like(d_src), torch.empty((h, w), dtype=torch.float32, device="cuda")
+    bf, abf = vip.CudaBilateralFilter(w, h, 9), vip.CudaAdaptiveBilateralFilter(w, h, 9)
+    tf = vip.CudaBilateralTextureFilter(w, h, 9, 3)
+
+    def grad_hip():
+        vip.cuda_gradient(d_src, d_mag, w, h, 3)
+        torch.cuda.synchronize()  # the reference's call returns unsynchronised; its D2H syncs
+
+    rows = [
+        ("gradient", lambda: o.gradient(img, o.CPP), grad_hip),
+        ("bilateral filter", lambda: o.bilateral(img, 9, profile=o.CPP, threads=threads),
+         lambda: bf.bilateral_filter(d_src, d_dst)),
+        ("adaptive bilateral filter", lambda: o.adaptive(img, 9, profile=o.CPP, threads=threads),
+         lambda: abf.execute(d_src, d_dst)),
+        ("bilateral texture filter", lambda: o.texture(img, 9, 3, o.CPP), lambda: tf.execute(d_src, d_dst)),
+    ]
+
+    def measure(fn, n=10):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        return (time.perf_counter() - t0) / n * 1e3
+
+    print(f"Parameters\n\twidth {w} height {h} execute times 10 ksize 9 texture ksize 9 nitr 3 "
+          f"(cpp: {threads} threads, {model})\n")
+    for name, cpp, hip in rows:
+        print(f"{name + ' [cpp]':40s} : {measure(cpp):10.6f} [msec]")
+        print(f"{name + ' [hip]':40s} : {measure(hip):10.6f} [msec]")
+
+
 def main():
     args = parse()
+    if args.sample_table:
+        sample_table(args)
+        return
     import torch
     import torch.distributed as dist
 

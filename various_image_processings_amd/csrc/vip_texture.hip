@@ -351,6 +351,16 @@ __device__ unsigned long long vip_gf_stamps[4096 * 16 * 16];
 #define VIP_GF_STAMP(k)
 #endif
 
+// Progress-based wave priority inside the long phases (set_progress_priority in
+// vip_stencil.hpp): band 0..3 as the thread advances through its gradients, pass-3 rows
+// and guide outputs, so the waves of a workgroup reach each phase barrier together.
+// Measured 733 -> 714 us per 4K k=5 nitr=5 frame (profiles/r02_variants.txt).
+#ifndef VIP_GF_NO_PRIO
+#define VIP_GF_PROGRESS(band) set_progress_priority(band)
+#else
+#define VIP_GF_PROGRESS(band)
+#endif
+
 // Row bands: rows [lo, hi) of the (dense, width*3 pitch) buffers are the valid
 // frame rows -- every stage clamps into them, as the reference clamps into
 // [0, height) -- and guide rows [gy0, gy1) are produced (a row slab of a sharded
@@ -433,6 +443,7 @@ VIP_GF_STAMP(8);
     float mrv[KM];  // this thread's gradients, stored to MR (over XR) after pass 1
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
+        VIP_GF_PROGRESS(k * 4 / KM);
         const int i = tid + k * G::NT;
         if (NM % G::NT != 0 && i >= NM) continue;
         const int qy = i / G::MW, qx = i - qy * G::MW;
@@ -484,6 +495,7 @@ VIP_GF_STAMP(8);
     }
     VIP_GF_STAMP(2);
     __syncthreads();  // XR is consumed (gradients and pass 1): MR takes its place
+    VIP_GF_PROGRESS(0);
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
         const int i = tid + k * G::NT;
@@ -536,6 +548,7 @@ VIP_GF_STAMP(8);
             win_op<kGfV2, K>(hmx, smx, pk_max_u16);
 #pragma unroll
             for (int t = 0; t < NV; ++t) {
+                VIP_GF_PROGRESS(t * 4 / NV);
                 const float* mrow = MR + (p0 + t) * G::MW + c;
                 float m[K];
 #pragma unroll
@@ -656,6 +669,7 @@ VIP_GF_STAMP(8);
         }
 #pragma unroll
         for (int j = 0; j < kGfRun; ++j) {
+            VIP_GF_PROGRESS(j * 4 / kGfRun);
             const int y = y0 + ty0 + j;
             if (y >= gy1) break;
             float rmin = CPP ? 3.402823466e+38f : 1e10f;
