@@ -411,28 +411,25 @@ def main():
             sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
 
     # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time.
-    # N>1: the halo exchange sits between kernels, so every KSAMPLE-th step is
-    # bracketed by events before the exchange, between exchange and kernel(s), and
-    # after them (an event pair costs ~11 us of stream time, measured with rocprofv3,
-    # so not every step carries them): exchange_ms and kernel_ms per rank.
-    KSAMPLE = 4
-    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range((args.steps + KSAMPLE - 1) // KSAMPLE)]
-    timed = {"on": False, "i": 0, "n": 0}
+    # N>1: the halo exchange sits between kernels; the timed steps carry no inner events
+    # (an event between launches costs stream time, ~11 us per pair measured with
+    # rocprofv3), so max(4, K/4) further steps after the timed region are bracketed by
+    # events before the exchange, between exchange and kernel(s), and after them:
+    # exchange_ms and kernel_ms per rank.
+    marks = []
 
-    def step(i):
-        sample = timed["on"] and world > 1 and timed["i"] % KSAMPLE == 0
+    def step(i, sample=False):
         if sample:
-            marks[timed["n"]][0].record(stream)
+            m = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            m[0].record(stream)
         if world > 1:
             exchange_halo(srcs[i % NBUF], geo)
         if sample:
-            marks[timed["n"]][1].record(stream)
+            m[1].record(stream)
         run(i)
         if sample:
-            marks[timed["n"]][2].record(stream)
-            timed["n"] += 1
-        if timed["on"]:
-            timed["i"] += 1
+            m[2].record(stream)
+            marks.append(m)
 
     # clock settle (untimed): steps for --settle-s seconds of wall time, checked every
     # few steps with a device sync; then the W warm-up steps
@@ -449,7 +446,6 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    timed["on"] = True
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -462,10 +458,12 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     exchange_ms = None
-    if timed["n"] > 0:
-        n = timed["n"]
-        exchange_ms = sum(m[0].elapsed_time(m[1]) for m in marks[:n]) / n
-        kernel_ms = sum(m[1].elapsed_time(m[2]) for m in marks[:n]) / n
+    if world > 1:
+        for i in range(max(4, args.steps // 4)):
+            step(args.warmup + args.steps + i, sample=True)
+        torch.cuda.synchronize(dev)
+        exchange_ms = sum(m[0].elapsed_time(m[1]) for m in marks) / len(marks)
+        kernel_ms = sum(m[1].elapsed_time(m[2]) for m in marks) / len(marks)
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
     stage_ms = None
@@ -535,7 +533,7 @@ def main():
                    **({"backend": args.backend} if world > 1 else {})},
         "roofline": roof,
         # per step, max over ranks: the kernel(s) and, at N>1, the halo exchange before
-        # them (event-timed on the filter stream every 4th step)
+        # them (event-timed on the filter stream in max(4, K/4) steps after the timed region)
         "kernel_ms": round(kernel_ms, 4),
         "settle": {"seconds": args.settle_s, "steps": settle_steps},
         **({"exchange_ms": round(exchange_ms, 4)} if exchange_ms is not None else {}),
