@@ -34,13 +34,25 @@ def _check_bands(got_rows, want_rows, spans):
         assert np.array_equal(g, w), (r0, n, _mismatch(g, w))
 
 
-def test_c3_adaptive_4k(dev, oracle):
+@pytest.mark.parametrize("numerics", [0, 1])
+def test_c3_adaptive_4k(dev, oracle, numerics):
     img = oracle.random_image(3840, 2160)
-    f = vip.CudaAdaptiveBilateralFilter(3840, 2160, 15)
+    f = vip.CudaAdaptiveBilateralFilter(3840, 2160, 15, numerics=numerics)
     d_dst = dev.empty(img.shape)
     f.execute(dev.put(img), d_dst)
     got = dev.get(d_dst)
-    want = oracle.bands(lambda r0, n: oracle.adaptive_rows(img, r0, n, 15), BANDS_4K)
+    want = oracle.bands(lambda r0, n: oracle.adaptive_rows(img, r0, n, 15, profile=numerics), BANDS_4K)
+    _check_bands([got[r0:r0 + n] for r0, n in BANDS_4K], want, BANDS_4K)
+
+
+@pytest.mark.parametrize("numerics", [0, 1])
+def test_c2_bilateral_4k_profiles(dev, oracle, numerics):
+    img = oracle.random_image(3840, 2160)
+    f = vip.CudaBilateralFilter(3840, 2160, 15, numerics=numerics)
+    d_dst = dev.empty(img.shape)
+    f.bilateral_filter(dev.put(img), d_dst)
+    got = dev.get(d_dst)
+    want = oracle.bands(lambda r0, n: oracle.bilateral_rows(img, r0, n, 15, profile=numerics), BANDS_4K)
     _check_bands([got[r0:r0 + n] for r0, n in BANDS_4K], want, BANDS_4K)
 
 
@@ -58,14 +70,15 @@ def test_joint_bilateral_4k(dev, oracle, k, ss, sc):
     _check_bands([got[r0:r0 + n] for r0, n in BANDS_4K], want, BANDS_4K)
 
 
-def test_c4_texture_4k(dev, oracle):
+@pytest.mark.parametrize("numerics", [0, 1])
+def test_c4_texture_4k(dev, oracle, numerics):
     img = oracle.random_image(3840, 2160)
-    f = vip.CudaBilateralTextureFilter(3840, 2160, 5, 5)
+    f = vip.CudaBilateralTextureFilter(3840, 2160, 5, 5, numerics=numerics)
     d_dst = dev.empty(img.shape)
     f.execute(dev.put(img), d_dst)
     got = dev.get(d_dst)
     spans = [(0, 16), (1016, 24), (2144, 16)]
-    want = oracle.bands(lambda r0, n: oracle.texture_rows(img, r0, n, 5, 5), spans)
+    want = oracle.bands(lambda r0, n: oracle.texture_rows(img, r0, n, 5, 5, profile=numerics), spans)
     _check_bands([got[r0:r0 + n] for r0, n in spans], want, spans)
 
 

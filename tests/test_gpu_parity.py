@@ -424,3 +424,40 @@ def test_bilateral_extreme_sigmas(dev, oracle, k, ss, sc):
         got = _bilateral_gpu(dev, img, k, ss, sc, guide=guide)
         want = oracle.bilateral(img, k, ss, sc) if guide is None else oracle.joint_bilateral(img, guide, k, ss, sc)
         assert np.array_equal(got, want), _mismatch(got, want)
+
+
+def test_texture_run_timed_matches_execute(dev, oracle):
+    """vip_texture_run_timed (the bench's per-stage timing entry point) produces the same
+    bytes as vip_texture_run and records 2 * nitr + 1 ordered events."""
+    import torch
+    img = oracle.random_image(200, 150)
+    t = _TextureImpl(200, 150, 5, 3)
+    d_src, a, b = dev.put(img), dev.empty(img.shape), dev.empty(img.shape)
+    t.execute(d_src, a)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(7)]
+    t.execute_timed(d_src, b, ev)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert np.array_equal(dev.get(b), oracle.texture(img, 5, 3))
+    assert all(ev[i].elapsed_time(ev[i + 1]) >= 0 for i in range(6))
+    with pytest.raises(ValueError):
+        t.execute_timed(d_src, b, ev[:6])
+
+
+def test_device_buffer_validation(dev):
+    """filters._ptr rejects wrong dtype, short buffers and host tensors with a Python
+    error instead of handing the kernels out-of-bounds pointers."""
+    import torch
+    f = vip.CudaBilateralFilter(64, 32, 9)
+    good = dev.empty((32, 64, 3))
+    with pytest.raises(ValueError):
+        f.bilateral_filter(dev.empty((31, 64, 3)), good)           # too few rows
+    with pytest.raises(ValueError):
+        f.bilateral_filter(torch.zeros((32, 64, 3), dtype=torch.float32, device="cuda"), good)  # dtype
+    with pytest.raises(ValueError):
+        f.bilateral_filter(torch.zeros((32, 64, 3), dtype=torch.uint8), good)  # host tensor
+    with pytest.raises(ValueError):
+        f.bilateral_filter(dev.empty((32, 128, 3))[:, ::2], good)  # not dense
+    impl = _BilateralImpl(64, 32, 9)
+    with pytest.raises(vip.VipError):  # C ABI: row range outside the handle's rows
+        impl.run_rows(dev.empty((40, 64, 3)), good, 8, 0, 0, 40)
