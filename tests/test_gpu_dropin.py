@@ -81,3 +81,70 @@ def test_sample_benchmark_outputs_match_oracle(tmp_path, oracle):
         for b in ref.tobytes():
             hsh = ((hsh ^ b) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
         assert f"{hsh:016x}" in out, (name, out)
+
+
+# ---- samples/vip_filter: image file -> drop-in C++ API -> image file ----------------
+# The per-filter samples of the reference (sample/{bilateral_filter, adaptive_bilateral_
+# filter, bilateral_texture_filter, gradient}/main.cpp) on lenna, read and written as PNG
+# by samples/vip_image_io.hpp; every output file must hold the oracle's bytes.
+def _read_ppm_bgr(path):
+    b = open(path, "rb").read()
+    magic, dims, maxv, raster = b.split(b"\n", 3)
+    w, h = map(int, dims.split())
+    c = 3 if magic == b"P6" else 1
+    a = np.frombuffer(raster, np.uint8).reshape(h, w, c)
+    return a[..., ::-1] if c == 3 else a[..., 0]
+
+
+@pytest.fixture(scope="module")
+def lenna_png(tmp_path_factory, lenna):
+    d = tmp_path_factory.mktemp("vip_filter")
+    ppm = d / "lenna.ppm"
+    ppm.write_bytes(b"P6\n512 512\n255\n" + np.ascontiguousarray(lenna[..., ::-1]).tobytes())
+    _run([os.path.join(ROOT, "samples", "vip_filter"), "convert", str(ppm), str(d / "lenna.png")])
+    flipped = d / "guide.ppm"  # joint filter guide: lenna mirrored left-right
+    flipped.write_bytes(b"P6\n512 512\n255\n" + np.ascontiguousarray(lenna[:, ::-1, ::-1]).tobytes())
+    return d
+
+
+@pytest.mark.parametrize("mode,params", [
+    ("bilateral", ["11", "10", "30"]),  # C1: lenna, ksize 11
+    ("bilateral", []),                  # the sample's defaults: ksize 9, sigma 10 / 30
+    ("joint", ["9", "10", "30"]),
+    ("adaptive", ["15", "10", "30"]),
+    ("texture", []),                    # defaults: ksize 9, nitr 3
+    ("texture", ["5", "5"]),            # C4's parameters
+])
+def test_vip_filter_image_files(lenna_png, lenna, oracle, mode, params):
+    exe = os.path.join(ROOT, "samples", "vip_filter")
+    src = lenna_png / "lenna.png"
+    out = lenna_png / f"{mode}_{'_'.join(params) or 'default'}.png"
+    args = [exe, mode, str(src)] + ([str(lenna_png / "guide.ppm")] if mode == "joint" else []) + [str(out)] + params
+    _run(args)
+    back = lenna_png / (out.stem + ".ppm")
+    _run([exe, "convert", str(out), str(back)])
+    got = _read_ppm_bgr(back)
+    p = [float(x) for x in params]
+    if mode == "bilateral":
+        want = oracle.bilateral(lenna, int(p[0]) if p else 9, *(p[1:] or [10.0, 30.0]), threads=8)
+    elif mode == "joint":
+        want = oracle.joint_bilateral(lenna, np.ascontiguousarray(lenna[:, ::-1]), int(p[0]), p[1], p[2], threads=8)
+    elif mode == "adaptive":
+        want = oracle.adaptive(lenna, int(p[0]), p[1], p[2], threads=8)
+    else:
+        want = oracle.texture(lenna, int(p[0]) if p else 9, int(p[1]) if p else 3)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_vip_filter_gradient(lenna_png, lenna, oracle):
+    exe = os.path.join(ROOT, "samples", "vip_filter")
+    raw = lenna_png / "grad.f32"
+    _run([exe, "gradient", str(lenna_png / "lenna.png"), str(raw)])
+    mag = np.fromfile(raw, np.float32).reshape(512, 512)
+    want = oracle.gradient(lenna)
+    np.testing.assert_array_equal(mag, want)
+    # the sample's display image: mag * float(255 / max), rounded half to even, saturated
+    _run([exe, "gradient", str(lenna_png / "lenna.png"), str(lenna_png / "grad.pgm"), "--repeat", "3"])
+    scale = np.float32(255.0 / float(want.max()))
+    disp = np.clip(np.rint(want * scale), 0, 255).astype(np.uint8)
+    np.testing.assert_array_equal(_read_ppm_bgr(lenna_png / "grad.pgm"), disp)
