@@ -95,6 +95,9 @@ def parse():
     # the reference's sample/benchmark table instead of the contract line
     p.add_argument("--sample-table", action="store_true")
     p.add_argument("--sample-size", default="100x100")
+    # c4 at N=1: two launches per iteration (default, faster) or the guide + JBF fused
+    # into one launch (include/vip.h vip_texture_set_mode)
+    p.add_argument("--texture-mode", default="two-launch", choices=["two-launch", "fused"])
     return p.parse_args()
 
 
@@ -274,6 +277,26 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms)
     return out
 
 
+def texture_fused_roofline(cfg: dict, px: int, frame_ms: float) -> dict:
+    """C4 in FUSED mode: one launch per iteration (texture_iteration_fused_kernel), so the
+    kernel is the whole iteration: FP32 rate of its JBF taps (8 FLOP per in-disc tap, the
+    guide stage's work beside it uncounted), VALU issue and HBM traffic from the
+    committed PMC summary of this mode (profiles/r*_c4fused_pmc.json)."""
+    nitr, k = cfg["nitr"], cfg["ksize"]
+    taps = circle_taps(k - 1)
+    launch_ms = frame_ms / nitr
+    kern = "void vip::texture_iteration_fused_kernel"
+    tf = 8.0 * taps * px / (launch_ms * 1e-3) / 1e12
+    traffic, tsrc = pmc_traffic("c4fused", [kern])
+    return dict(kernel=f"texture_iteration_fused_kernel (guide + JBF ksize {2 * k - 1} in one launch)",
+                avg_launch_ms=round(launch_ms, 4), bound="valu-fp32", achieved=round(tf, 3), peak=PEAK_FP32_TFLOPS,
+                unit="TFLOP/s", frac=round(tf / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
+                traffic_algorithmic=6.0 * px, valu_issue=valu_issue("c4fused", kern, launch_ms),
+                pipeline=dict(frame_ms=round(frame_ms, 4), launches=nitr,
+                              traffic_per_frame=traffic * nitr if traffic else None,
+                              fused_floor_bytes=6.0 * px * nitr))
+
+
 def sample_table(args) -> None:
     """The reference's sample/benchmark/main.cpp:105-213 table: every filter timed on the
     include/cpp path and on the GPU path side by side, on a randu(100, 120) image of
@@ -375,6 +398,8 @@ def main():
         frame_h = rows
         geo = None
         tex = _TextureImpl(w, rows, k, cfg["nitr"])
+        if args.texture_mode == "fused":
+            tex.set_mode(_TextureImpl.FUSED)
         srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         smarks = []
@@ -467,7 +492,8 @@ def main():
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
     stage_ms = None
-    if cfg["kind"] == "texture" and world == 1:
+    fused = cfg["kind"] == "texture" and world == 1 and args.texture_mode == "fused"
+    if cfg["kind"] == "texture" and world == 1 and not fused:
         # Per-stage split of the frame: an event between two launches costs a few us of
         # stream time (measured: +4 us on each stage against rocprofv3), so the timed
         # frames above carry no inner events; max(4, K/4) further frames, after the
@@ -494,7 +520,9 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = total_px / (elapsed / args.steps) / 1e6
 
-    if cfg["kind"] == "texture":
+    if fused:
+        roof = texture_fused_roofline(cfg, px_per_rank, kernel_ms)
+    elif cfg["kind"] == "texture":
         roof = texture_roofline(args.config, cfg, px_per_rank, kernel_ms, stage_ms)
     else:
         taps = circle_taps(r)
@@ -530,6 +558,7 @@ def main():
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows,
                    "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
+                   **({"texture_mode": args.texture_mode} if cfg["kind"] == "texture" and world == 1 else {}),
                    **({"backend": args.backend} if world > 1 else {})},
         "roofline": roof,
         # per step, max over ranks: the kernel(s) and, at N>1, the halo exchange before

@@ -122,6 +122,17 @@ int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void*
  * before its joint bilateral, events[2*nitr] after the last launch. */
 int vip_texture_run_timed(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream, void* const* events);
 
+/* Iteration form (no reference counterpart; same bytes either way). TWO_LAUNCH (the
+ * default): per iteration the fused guide stage writes the guide frame to HBM and the
+ * joint bilateral reads it -- src/bilateral_texture_filter_impl.cu:207-210's four stages
+ * in two launches. FUSED (ksize 5 only, else VIP_ERR_UNSUPPORTED_KSIZE): one launch per
+ * iteration, the guide of each JBF tile computed in LDS with the JBF apron (SURVEY
+ * §8(f)1); vip_texture_run_timed's events[2i+1] then follows the whole iteration. The
+ * row-slab entry point below always uses TWO_LAUNCH. */
+#define VIP_TEXTURE_TWO_LAUNCH 0
+#define VIP_TEXTURE_FUSED 1
+int vip_texture_set_mode(vip_texture_t h, int mode);
+
 /* Row-slab form of one texture iteration for a row-sharded frame (SURVEY §8(f)3;
  * the reference is single-GPU). d_src is a dense slab of the handle's width x
  * height (pitch width*3) whose rows [row_lo, row_hi) are valid frame rows: every

@@ -4,7 +4,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 CFG=${1:-c2}
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$CFG -o run --output-format csv -- python bench.py --config $CFG --steps 10 --no-cpu-baseline > gpurun_out/prof_$CFG.log 2>&1
+ARGS="--config $CFG"
+[ "$CFG" = c4fused ] && ARGS="--config c4 --texture-mode fused"  # C4, guide + JBF in one launch
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$CFG -o run --output-format csv -- python bench.py $ARGS --steps 10 --no-cpu-baseline > gpurun_out/prof_$CFG.log 2>&1
 rc=$?; echo "rocprof $CFG rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python - "$CFG" <<'PY'
 import csv, sys

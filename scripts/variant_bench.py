@@ -26,6 +26,14 @@ cases += [("joint_r4", lambda s, d: j9.joint_bilateral_filter(s, guide, d)),
           ("joint_r7", lambda s, d: j15.joint_bilateral_filter(s, guide, d)),
           ("texture_k5_nitr1", _TextureImpl(W, H, 5, 1).execute),
           ("texture_k5_nitr5", _TextureImpl(W, H, 5, 5).execute)]
+def fused(nitr):  # vip_texture_set_mode(FUSED): guide + JBF in one launch per iteration
+    t = _TextureImpl(W, H, 5, nitr)
+    t.set_mode(_TextureImpl.FUSED)
+    return t.execute
+try:
+    cases += [("texture_k5_nitr1_fused", fused(1)), ("texture_k5_nitr5_fused", fused(5))]
+except Exception:  # an older library without the mode
+    pass
 if "--r15" in sys.argv:  # one 2048-row slab of the C5 frame (16384 wide, ksize 31)
     s15 = [torch.randint(0, 255, (2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
     d15 = torch.empty((2048 + 30, 16384, 3), dtype=torch.uint8, device="cuda")

@@ -168,6 +168,34 @@ def test_texture_end_to_end(dev, oracle, shape, k, nitr, numerics, profile):
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
+# FUSED mode (include/vip.h vip_texture_set_mode): guide + JBF of an iteration in one
+# launch, the guide kept in LDS; k = 5 only. Ragged shapes cross every tile border case
+# (plane positions outside the frame on each side, partial tiles, one-tile frames).
+@pytest.mark.parametrize("shape,nitr", [((48, 64), 5), ((50, 50), 3), ((121, 203), 3), ((7, 9), 2), ((1, 1), 1),
+                                        ((65, 129), 2), ((200, 300), 2), ((530, 700), 1)])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_texture_fused_mode(dev, oracle, shape, nitr, numerics, profile):
+    h, w = shape
+    img = oracle.random_u8(h * w * 3).reshape(h, w, 3)
+    t = _TextureImpl(w, h, 5, nitr, numerics)
+    t.set_mode(_TextureImpl.FUSED)
+    d_dst = dev.empty((h, w, 3))
+    t.execute(dev.put(img), d_dst)
+    got, want = dev.get(d_dst), oracle.texture(img, 5, nitr, profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+    d = dev.put(img)  # in place
+    t.execute(d, d)
+    assert np.array_equal(dev.get(d), want)
+
+
+def test_texture_fused_mode_errors(dev):
+    t = _TextureImpl(64, 48, 9, 1)
+    with pytest.raises(vip.VipError):  # fused is ksize 5 only
+        t.set_mode(_TextureImpl.FUSED)
+    with pytest.raises(vip.VipError):
+        _TextureImpl(64, 48, 5, 1).set_mode(7)
+
+
 def test_texture_in_place_and_zero_iterations(dev, oracle):
     img = oracle.random_image(40, 30)
     f = vip.CudaBilateralTextureFilter(40, 30, 5, 1)

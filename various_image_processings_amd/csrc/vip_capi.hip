@@ -38,6 +38,7 @@ int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, in
                                hipStream_t stream);
 int launch_texture_guide_fused_rows(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
                                     int ksize, bool cpp, hipStream_t stream);
+int launch_texture_iteration_fused(const StencilArgs& a, int ksize, bool cpp, hipStream_t stream);
 
 // LUT construction. CUDA profile: src/bilateral_filter_impl.cu:217-237 (float
 // coefficient, std::exp(float) == expf). CPP profile: include/cpp/bilateral_filter.hpp:13-36
@@ -122,6 +123,7 @@ struct vip_adaptive_s {
 
 struct vip_texture_s {
     int width, height, ksize, nitr, numerics;
+    int mode;  // VIP_TEXTURE_TWO_LAUNCH or VIP_TEXTURE_FUSED (vip_texture_set_mode)
     vip_bilateral_t jbf;
     uint8_t* d_ping[2];
     uint8_t* d_guide;
@@ -373,6 +375,13 @@ int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int
     return 0;
 }
 
+int vip_texture_set_mode(vip_texture_t h, int mode) {
+    if (!h || (mode != VIP_TEXTURE_TWO_LAUNCH && mode != VIP_TEXTURE_FUSED)) return VIP_ERR_INVALID_ARGUMENT;
+    if (mode == VIP_TEXTURE_FUSED && h->ksize != 5) return VIP_ERR_UNSUPPORTED_KSIZE;
+    h->mode = mode;
+    return 0;
+}
+
 int vip_texture_blur_rtv(vip_texture_t h, const uint8_t* d_image, const float* d_magnitude, float* d_blurred,
                          float* d_rtv, void* stream) {
     if (!h || !d_image || !d_magnitude || !d_blurred || !d_rtv) return VIP_ERR_INVALID_ARGUMENT;
@@ -405,10 +414,20 @@ static int texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, vo
         uint8_t* next = (it == h->nitr - 1) ? d_dst : (cur == h->d_ping[0] ? h->d_ping[1] : h->d_ping[0]);
         // gradient -> blur/mRTV -> guide fused in LDS (one launch), then the JBF
         if (events) VIP_HIP_CHECK(hipEventRecord((hipEvent_t)events[2 * it], s));
-        int rc = launch_texture_guide_fused(cur, h->d_guide, h->width, h->height, h->ksize,
+        int rc;
+        if (h->mode == VIP_TEXTURE_FUSED) {  // guide + JBF in one launch, the guide stays in LDS
+            const vip_bilateral_s* j = h->jbf;
+            StencilArgs a;
+            fill_args(a, h->width, cur, pitch, cur, pitch, next, pitch, h->height, 0, 0, h->height, j->d_color,
+                      j->lut_nonzero, nullptr, j->wsq);
+            rc = launch_texture_iteration_fused(a, h->ksize, h->numerics == VIP_NUMERICS_CPP, s);
+            if (!rc && events) rc = (int)hipEventRecord((hipEvent_t)events[2 * it + 1], s);
+        } else {
+            rc = launch_texture_guide_fused(cur, h->d_guide, h->width, h->height, h->ksize,
                                             h->numerics == VIP_NUMERICS_CPP, s);
-        if (!rc && events) rc = (int)hipEventRecord((hipEvent_t)events[2 * it + 1], s);
-        if (!rc) rc = vip_joint_bilateral_run(h->jbf, cur, pitch, h->d_guide, pitch, next, pitch, stream);
+            if (!rc && events) rc = (int)hipEventRecord((hipEvent_t)events[2 * it + 1], s);
+            if (!rc) rc = vip_joint_bilateral_run(h->jbf, cur, pitch, h->d_guide, pitch, next, pitch, stream);
+        }
         if (rc) return rc;
         cur = next;
     }

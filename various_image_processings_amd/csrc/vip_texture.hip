@@ -279,9 +279,9 @@ constexpr int kGfRun = 4;  // guide: vertically adjacent outputs per thread
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-template <int R>
-struct GfGeom {
-    static constexpr int TW = gf_tile(R).tw, TH = gf_tile(R).th, NT = gf_tile(R).nt;
+template <int R, int TW_, int TH_, int NT_>
+struct GfGeomT {
+    static constexpr int TW = TW_, TH = TH_, NT = NT_;
     static_assert(TW % 4 == 0 && TH % 4 == 0, "guide tile: 4-pixel groups, 4-row runs");
     static constexpr int K = 2 * R + 1;
     static constexpr int BW = TW + 2 * R;               // BR/RR: T (+) R
@@ -306,6 +306,8 @@ struct GfGeom {
     static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
     static constexpr int IT2 = (NR2 + NT - 1) / NT;
 };
+template <int R>
+using GfGeom = GfGeomT<R, gf_tile(R).tw, gf_tile(R).th, gf_tile(R).nt>;
 
 typedef short gf_s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short gf_u16x2 __attribute__((ext_vector_type(2)));
@@ -365,24 +367,23 @@ __device__ unsigned long long vip_gf_stamps[4096 * 16 * 16];
 // frame rows -- every stage clamps into them, as the reference clamps into
 // [0, height) -- and guide rows [gy0, gy1) are produced (a row slab of a sharded
 // frame; the whole frame is lo = gy0 = 0, hi = gy1 = height).
-template <int R, bool CPP>
-__global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
-                                                                   uint8_t* __restrict__ guide, int width, int lo,
-                                                                   int hi, int gy0, int gy1, int ksize,
-                                                                   int aligned) {
-    using G = GfGeom<R>;
+// Phases 1-4 of one guide tile: G::TW x G::TH guide outputs with origin (x0, y0) in
+// image coordinates, from the image rows [lo, hi) (every read clamps into them) in
+// the G::WORDS words of LDS at `lds`; rows >= gy1 and columns past the image are not
+// produced. Each guide word (RGBX) goes to sink(ty, tx, word), tile-relative. Ends
+// after the guide phase WITHOUT a barrier (the caller's sink target decides).
+template <class G, int R, bool CPP, class Sink>
+__device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restrict__ img, int width, int lo, int hi,
+                                           int gy1, int ksize, int aligned, int x0, int y0, Sink&& sink) {
     constexpr int K = G::K;  // window width; the reference divides by ksize^2 and
                              // uses sigma_alpha = 1/(5 ksize) even when ksize is even
     constexpr bool PACKRB = K * K * 255 < 65536;  // R|B<<16 vertical sums stay in 16 bits
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* XR = lds;
     uint32_t* H = lds + G::XR_WORDS;                    // RB plane, MX plane (HPL words each)
     uint16_t* HG = reinterpret_cast<uint16_t*>(H + 2 * G::HPL);  // G sums (<= K * 255) as u16
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
     float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
-    const int x0 = blockIdx.x * G::TW, y0 = gy0 + blockIdx.y * G::TH;
-    VIP_GF_STAMP(0);
     const int tid = threadIdx.x;
     // region origins (image coordinates)
     const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
@@ -645,7 +646,6 @@ VIP_GF_STAMP(8);
     //    found once and shared; scanning those rows in order with strict > then
     //    gives the row-major first argmin. Alpha blend per output.
     const float sigma_alpha = 1.f / (float)(5 * ksize);
-    uint32_t* GT = lds + 4 * G::BPL;  // guide tile as RGBX words, after BR/RR
     for (int run = tid; run < (G::TH / kGfRun) * G::TW; run += G::NT) {
         const int tx = run % G::TW, ty0 = (run / G::TW) * kGfRun;
         const int x = x0 + tx;
@@ -699,9 +699,25 @@ VIP_GF_STAMP(8);
                 const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
                 gw |= (uint32_t)clampi((int)v, 0, 255) << (8 * c);
             }
-            GT[(ty0 + j) * G::TW + tx] = gw;
+            sink(ty0 + j, tx, gw);
         }
     }
+}
+
+template <int R, bool CPP>
+__global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
+                                                                   uint8_t* __restrict__ guide, int width, int lo,
+                                                                   int hi, int gy0, int gy1, int ksize,
+                                                                   int aligned) {
+    using G = GfGeom<R>;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int x0 = blockIdx.x * G::TW, y0 = gy0 + blockIdx.y * G::TH;
+    const int tid = threadIdx.x;
+    const int W1 = width - 1;
+    VIP_GF_STAMP(0);
+    uint32_t* GT = lds + 4 * G::BPL;  // guide tile as RGBX words, after BR/RR
+    guide_tile<G, R, CPP>(lds, img, width, lo, hi, gy1, ksize, aligned, x0, y0,
+                          [&](int ty, int tx, uint32_t gw) { GT[ty * G::TW + tx] = gw; });
     VIP_GF_STAMP(6);
     __syncthreads();
 
@@ -775,6 +791,139 @@ int launch_texture_guide_fused_rows(const uint8_t* img, uint8_t* guide, int widt
 int launch_texture_guide_fused(const uint8_t* img, uint8_t* guide, int width, int height, int ksize, bool cpp,
                                hipStream_t stream) {
     return launch_texture_guide_fused_rows(img, guide, width, 0, height, 0, height, ksize, cpp, stream);
+}
+
+// ---------------------------------------------------------------------------
+// One whole bilateral-texture iteration in one launch (guide + JBF fused
+// in LDS), ksize 5 (C4) only: each workgroup owns a 128 x 64 tile of JBF outputs, the
+// stencil kernel's tile (16 waves, 8 outputs per thread, JBF radius 4). It computes the
+// guide over the tile (+) 4 -- 136 x 72 positions, in three 136 x 24 chunks through
+// guide_tile -- straight into the JBF's guide plane, replaces every plane position
+// outside the image by the guide at its clamped position (what the two-launch JBF reads
+// through its clamped coordinates), loads the image plane (L2-hot: the guide just read
+// it) and the 16-copy colour LUT into the chunks' dead scratch, and runs the JBF taps of
+// bilateral_kernel. The guide never reaches HBM: 3 B/px read (+ halo) and 3 B/px
+// written per iteration. The price is 1.2x the guide work (the 4-pixel JBF apron) and
+// one workgroup per CU (127 KiB of LDS). Same arithmetic as the two launches, so the
+// same bytes; selected per handle (vip_texture_set_mode).
+// ---------------------------------------------------------------------------
+constexpr int kFuR = 2, kFuJR = 4, kFuP = 8, kFuWaves = 16, kFuNT = kFuWaves * 64;
+constexpr int kFuTH = kFuWaves * 4;            // 64 output rows
+constexpr int kFuRows = kFuTH + 2 * kFuJR;     // 72 guide / image plane rows
+constexpr int kFuChunk = 24;                   // guide rows per guide_tile call
+constexpr int kFuCopies = 16;
+using FuJG = Geom<kFuJR, kFuP>;                // TW 128, L 4, S 140
+using FuGG = GfGeomT<kFuR, FuJG::TW + 2 * kFuJR, kFuChunk, kFuNT>;
+constexpr int kFuPlane = kFuRows * FuJG::S;
+constexpr int kFuLutWords = 768 * kFuCopies;
+constexpr int kFuScratch = cmax(FuGG::WORDS, kFuPlane + kFuLutWords);
+constexpr int kFuLds = 4 * (kFuPlane + kFuScratch);
+static_assert(FuJG::L == kFuJR && FuGG::TW == FuJG::TW + 2 * FuJG::L, "guide chunk covers the plane columns");
+static_assert(kFuRows % kFuChunk == 0 && FuJG::S >= FuGG::TW, "plane geometry");
+static_assert(kFuLds <= kLdsBudget, "fused iteration does not fit LDS");
+
+template <bool CPP>
+__global__ __launch_bounds__(kFuNT) void texture_iteration_fused_kernel(const StencilArgs a, int ksize) {
+    constexpr int R = kFuR, JR = kFuJR, P = kFuP, S = FuJG::S;
+    constexpr bool FMA = !CPP;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* const gplane = lds;
+    uint32_t* const scratch = lds + kFuPlane;
+    uint32_t* const splane = scratch;
+    uint32_t* const lut = scratch + kFuPlane;
+    const int tid = threadIdx.x;
+    const int tx0 = ((int)blockIdx.x % a.tiles_x) * FuJG::TW, ty0 = ((int)blockIdx.x / a.tiles_x) * kFuTH;
+    const int W1 = a.width - 1, lo = a.row_lo, hi = a.row_hi;
+    const int gx0 = tx0 - JR, gy0 = ty0 - JR;  // plane origin (image coordinates)
+    const int aligned = a.aligned ? 1 : 0;
+
+    // 1. guide over the plane, three chunks of rows; plane word (r, c) <-> (gx0 + c, gy0 + r)
+#pragma unroll 1
+    for (int c = 0; c < kFuRows / kFuChunk; ++c) {
+        if (c) __syncthreads();  // the previous chunk is done with the scratch
+        uint32_t* const prow = gplane + c * kFuChunk * S;
+        guide_tile<FuGG, R, CPP>(scratch, a.src, a.width, lo, hi, hi, ksize, aligned, gx0, gy0 + c * kFuChunk,
+                                 [&](int ty, int tx, uint32_t gw) { prow[ty * S + tx] = gw; });
+    }
+    __syncthreads();
+    // 2. plane positions outside the image take the guide at their clamped position
+    //    (reads in-image words, writes out-of-image words only: one pass, no hazard)
+    if (gx0 < 0 || gy0 < lo || gx0 + FuGG::TW > W1 + 1 || gy0 + kFuRows > hi) {
+        for (int q = tid; q < kFuRows * FuGG::TW; q += kFuNT) {
+            const int r = q / FuGG::TW, cc = q - r * FuGG::TW;
+            const int y = gy0 + r, x = gx0 + cc;
+            const int cy = clampi(y, lo, hi - 1), cx = clampi(x, 0, W1);
+            if (cy != y || cx != x) gplane[r * S + cc] = gplane[(cy - gy0) * S + (cx - gx0)];
+        }
+    }
+    // 3. image plane (pre-clamped, as the stencil kernel's TilePrefetch loads it) and the
+    //    colour LUT into the dead chunk scratch
+    {
+        TilePrefetch<JR, kFuRows, kFuNT, P> ps;
+        ps.issue(a.src, a.src_pitch, a, tx0, ty0);
+        stage_lut<kFuNT, 768, kFuCopies>(lut, a.color);
+        ps.commit(splane);
+    }
+    __syncthreads();
+
+    // 4. JBF taps: bilateral_kernel's loop with two planes (src = image, guide = plane)
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int tx = lane & 15;
+    const int ty = wave * 4 + (lane >> 4);
+    const uint32_t lane4 = (uint32_t)(lane & (kFuCopies - 1)) << 2;
+    const char* const lut_bytes = reinterpret_cast<const char*>(lut);
+    if (ty0 + wave * 4 >= a.out_rows) return;  // wave-uniform: rows past the frame
+    uint32_t ctr[P];
+    {
+        const uint4* cp = reinterpret_cast<const uint4*>(gplane + (ty + JR) * S + tx * P + FuJG::L);
+#pragma unroll
+        for (int q = 0; q < P / 4; ++q) {
+            const uint4 v = cp[q];
+            ctr[4 * q + 0] = v.x; ctr[4 * q + 1] = v.y; ctr[4 * q + 2] = v.z; ctr[4 * q + 3] = v.w;
+        }
+    }
+    f2 a01[P], a2k[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) a01[i] = a2k[i] = f2{0.f, 0.f};
+    for_each_row<JR, true>([&](const int ky, auto hwc) {
+        constexpr int HW = decltype(hwc)::value;
+        const int aky = ky < 0 ? -ky : ky;
+        set_progress_priority((ky + JR) * 4 / (2 * JR + 1));
+        const int row_off = (ty + JR + ky) * S + tx * P;
+        const float* const ws = a.ws + aky * kWsStride;
+        constexpr int C0 = (FuJG::L - HW) / 4, C1 = (FuJG::L + P - 1 + HW) / 4;
+        constexpr int NC = C1 - C0 + 1;
+        float wsv[HW + 1];
+#pragma unroll
+        for (int k = 0; k <= HW; ++k) wsv[k] = ws[k];
+        auto widx = [&](uint32_t g, f2, f2, int i, int) {
+            const uint32_t d = __builtin_amdgcn_sad_u8(g, ctr[i], 0u);
+            return (d << 6) | lane4;  // 16 copies: word d * 16 + copy
+        };
+        row_taps<HW, FuJG::L, C0, NC, FMA, false, P, true, decltype(widx)&>(gplane, splane, row_off, wsv, lut_bytes,
+                                                                            widx, a01, a2k);
+        fence_accumulators(a01, a2k);
+    });
+    uint32_t o[P];
+    finish_outputs<P, true>(a01, a2k, o);
+    store_px(a, ty0 + ty, tx0 + tx * P, o);
+}
+
+// One fused iteration of a whole frame (src -> dst, both dense pitch width*3; they must
+// not alias). `a` carries the JBF handle's LUTs and the frame geometry.
+int launch_texture_iteration_fused(const StencilArgs& a, int ksize, bool cpp, hipStream_t stream) {
+    if (ksize != 2 * kFuR + 1) return VIP_ERR_UNSUPPORTED_KSIZE;
+    auto kern = cpp ? texture_iteration_fused_kernel<true> : texture_iteration_fused_kernel<false>;
+    static std::atomic<unsigned long long> attr_devs[2];
+    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), kFuLds, attr_devs[cpp ? 1 : 0]))
+        return rc;
+    StencilArgs args = a;
+    args.tiles_x = (a.width + FuJG::TW - 1) / FuJG::TW;
+    args.tiles_total = args.tiles_x * ((a.out_rows + kFuTH - 1) / kFuTH);
+    if (args.tiles_total == 0) return 0;
+    hipLaunchKernelGGL(kern, dim3(args.tiles_total), dim3(kFuNT), kFuLds, stream, args, ksize);
+    return (int)hipGetLastError();
 }
 
 }  // namespace vip

@@ -177,6 +177,13 @@ class _TextureImpl(_Handle):
         call("vip_texture_create", ctypes.byref(self._h), self.width, self.height, self.ksize, self.nitr,
              int(numerics))
 
+    TWO_LAUNCH, FUSED = 0, 1  # include/vip.h VIP_TEXTURE_*
+
+    def set_mode(self, mode):
+        """TWO_LAUNCH (default) or FUSED (ksize 5: guide + JBF in one launch per
+        iteration, the guide kept in LDS); include/vip.h vip_texture_set_mode."""
+        call("vip_texture_set_mode", self._h, int(mode))
+
     def execute(self, d_src, d_dst, stream=None):
         n = self.width * self.height * 3
         call("vip_texture_run", self._h, _ptr(d_src, n), _ptr(d_dst, n), _stream(stream))
