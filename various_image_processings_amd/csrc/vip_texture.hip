@@ -372,7 +372,7 @@ __device__ unsigned long long vip_gf_stamps[4096 * 16 * 16];
 // the G::WORDS words of LDS at `lds`; rows >= gy1 and columns past the image are not
 // produced. Each guide word (RGBX) goes to sink(ty, tx, word), tile-relative. Ends
 // after the guide phase WITHOUT a barrier (the caller's sink target decides).
-template <class G, int R, bool CPP, class Sink>
+template <class G, int R, bool CPP, bool OPAQUE_TID = false, class Sink>
 __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restrict__ img, int width, int lo, int hi,
                                            int gy1, int ksize, int aligned, int x0, int y0, Sink&& sink) {
     constexpr int K = G::K;  // window width; the reference divides by ksize^2 and
@@ -384,7 +384,15 @@ __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restr
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
     float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
-    const int tid = threadIdx.x;
+    // OPAQUE_TID (the fused iteration kernel, which calls this three times): without it
+    // the compiler keeps chunk 0's thread-index arithmetic live across the later chunks
+    // (18 spilled VGPRs, ~90 MB of scratch writes per 4K launch); recomputing is cheaper.
+    // The single-call guide stage keeps the plain index (and its known range).
+    int tid = threadIdx.x;
+    if constexpr (OPAQUE_TID) {
+        __asm__ volatile("" : "+v"(tid));
+        __builtin_assume(tid >= 0 && tid < G::NT);
+    }
     // region origins (image coordinates)
     const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
     const int mr0x = x0 - 2 * R, mr0y = y0 - 2 * R;
@@ -838,11 +846,11 @@ __global__ __launch_bounds__(kFuNT) void texture_iteration_fused_kernel(const St
     const int aligned = a.aligned ? 1 : 0;
 
     // 1. guide over the plane, three chunks of rows; plane word (r, c) <-> (gx0 + c, gy0 + r)
-#pragma unroll 1
+#pragma unroll
     for (int c = 0; c < kFuRows / kFuChunk; ++c) {
         if (c) __syncthreads();  // the previous chunk is done with the scratch
         uint32_t* const prow = gplane + c * kFuChunk * S;
-        guide_tile<FuGG, R, CPP>(scratch, a.src, a.width, lo, hi, hi, ksize, aligned, gx0, gy0 + c * kFuChunk,
+        guide_tile<FuGG, R, CPP, true>(scratch, a.src, a.width, lo, hi, hi, ksize, aligned, gx0, gy0 + c * kFuChunk,
                                  [&](int ty, int tx, uint32_t gw) { prow[ty * S + tx] = gw; });
     }
     __syncthreads();
