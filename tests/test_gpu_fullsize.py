@@ -45,6 +45,27 @@ def test_c3_adaptive_4k(dev, oracle, numerics):
     _check_bands([got[r0:r0 + n] for r0, n in BANDS_4K], want, BANDS_4K)
 
 
+@pytest.mark.parametrize("kind", ["bilateral", "adaptive", "texture"])
+def test_reference_defaults_4k_natural_image(dev, oracle, lenna, kind):
+    """The reference samples' default parameters (ksize 9, sigma 10 / 30; texture ksize 9,
+    nitr 3: sample/*/main.cpp) on a 4K frame of natural-image statistics (lenna tiled,
+    SURVEY 8(d) input iii): small colour distances dominate, unlike uniform noise."""
+    img = np.ascontiguousarray(np.tile(lenna, (5, 8, 1))[:2160, :3840])
+    d_dst = dev.empty(img.shape)
+    if kind == "bilateral":
+        vip.CudaBilateralFilter(3840, 2160).bilateral_filter(dev.put(img), d_dst)
+        fn = lambda r0, n: oracle.bilateral_rows(img, r0, n, 9)  # noqa: E731
+    elif kind == "adaptive":
+        vip.CudaAdaptiveBilateralFilter(3840, 2160).execute(dev.put(img), d_dst)
+        fn = lambda r0, n: oracle.adaptive_rows(img, r0, n, 9)  # noqa: E731
+    else:
+        vip.CudaBilateralTextureFilter(3840, 2160).execute(dev.put(img), d_dst)
+        fn = lambda r0, n: oracle.texture_rows(img, r0, n, 9, 3)  # noqa: E731
+    got = dev.get(d_dst)
+    spans = [(0, 12), (508, 8), (2148, 12)]
+    _check_bands([got[r0:r0 + n] for r0, n in spans], oracle.bands(fn, spans), spans)
+
+
 @pytest.mark.parametrize("numerics", [0, 1])
 def test_c2_bilateral_4k_profiles(dev, oracle, numerics):
     img = oracle.random_image(3840, 2160)
