@@ -98,6 +98,12 @@ def parse():
     # c4 at N=1: two launches per iteration (default, faster) or the guide + JBF fused
     # into one launch (include/vip.h vip_texture_set_mode)
     p.add_argument("--texture-mode", default="two-launch", choices=["two-launch", "fused"])
+    # frames in flight: step i runs on HIP stream i % S (one filter handle per stream
+    # where the handle owns scratch), so one frame's kernel tails and launch gaps overlap
+    # the next frame's start. Measured (scripts/stream_bench.py, steady clocks): C2
+    # 0.178 -> 0.173 ms, C3 0.327 -> 0.323, C4 0.717 -> 0.641 ms per frame with 2; 3 no
+    # better. S must divide the 12 rotating buffers (a buffer always meets the same stream)
+    p.add_argument("--streams", type=int, default=2, choices=[1, 2, 3, 4, 6])
     return p.parse_args()
 
 
@@ -386,7 +392,10 @@ def main():
     from various_image_processings_amd.filters import _TextureImpl
     from various_image_processings_amd.sharded import ShardedBilateral, ShardedTexture, exchange_halo
 
-    stream = torch.cuda.current_stream(dev)
+    S = args.streams
+    # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    stream = streams[0]
     w = cfg["width"]
     k = cfg["ksize"]
     r = k // 2
@@ -397,71 +406,81 @@ def main():
         rows = cfg["rows_per_rank"]
         frame_h = rows
         geo = None
-        tex = _TextureImpl(w, rows, k, cfg["nitr"])
+        # one handle per stream: a texture handle owns its ping-pong and guide frames
+        texs = [_TextureImpl(w, rows, k, cfg["nitr"]) for _ in range(S)]
         if args.texture_mode == "fused":
-            tex.set_mode(_TextureImpl.FUSED)
+            for t_ in texs:
+                t_.set_mode(_TextureImpl.FUSED)
         srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         smarks = []
 
-        def run(i):
-            tex.execute(srcs[i % NBUF], dsts[i % NBUF], stream=stream)
+        def run(i, s=stream, h=0):
+            texs[h].execute(srcs[i % NBUF], dsts[i % NBUF], stream=s)
 
         def run_staged(i):
             """one frame with per-stage events (vip_texture_run_timed)"""
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * cfg["nitr"] + 1)]
-            tex.execute_timed(srcs[i % NBUF], dsts[i % NBUF], ev, stream=stream)
+            texs[0].execute_timed(srcs[i % NBUF], dsts[i % NBUF], ev, stream=stream)
             smarks.append(ev)
     elif cfg["kind"] == "texture":
         # row-sharded frame: one halo exchange of nitr * texture_halo_rows(k) rows per
-        # frame, then shrinking ghost zones (sharded.ShardedTexture)
+        # frame, then shrinking ghost zones (sharded.ShardedTexture; one per stream: it
+        # owns scratch slabs)
         frame_h = cfg["rows_per_rank"] * world
-        st = ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world)
-        geo = st.geo
+        sts = [ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world) for _ in range(S)]
+        geo = sts[0].geo
         rows = geo.own
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
-        def run(i):
-            st.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
+        def run(i, s=stream, h=0):
+            sts[h].filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
     else:
         frame_h = cfg.get("frame_height", cfg.get("rows_per_rank", 0) * world)
+        # the handle holds only read-only LUTs: one serves every stream
         sb = ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
         geo = sb.geo
         rows = geo.own
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
-        def run(i):
-            sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=stream, exchange=False)
+        def run(i, s=stream, h=0):
+            sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
 
-    # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time.
+    # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time per frame
+    # (with S > 1 streams: per frame with S frames in flight).
     # N>1: the halo exchange sits between kernels; the timed steps carry no inner events
     # (an event between launches costs stream time, ~11 us per pair measured with
-    # rocprofv3), so max(4, K/4) further steps after the timed region are bracketed by
-    # events before the exchange, between exchange and kernel(s), and after them:
-    # exchange_ms and kernel_ms per rank.
+    # rocprofv3), so max(4, K/4) further steps after the timed region, on one stream, are
+    # bracketed by events before the exchange, between exchange and kernel(s), and after
+    # them: exchange_ms and kernel_ms per rank.
     marks = []
 
     def step(i, sample=False):
-        if sample:
-            m = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            m[0].record(stream)
-        if world > 1:
-            exchange_halo(srcs[i % NBUF], geo)
-        if sample:
-            m[1].record(stream)
-        run(i)
-        if sample:
-            m[2].record(stream)
-            marks.append(m)
+        # step i on stream i % S; buffer i % NBUF therefore always meets the same stream
+        # (S divides NBUF), so a halo receive into it is ordered after its last reader
+        h = 0 if sample else i % S
+        s = streams[h]
+        with torch.cuda.stream(s):  # RCCL orders its P2P against the current stream
+            if sample:
+                m = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                m[0].record(s)
+            if world > 1:
+                exchange_halo(srcs[i % NBUF], geo)
+            if sample:
+                m[1].record(s)
+            run(i, s, h)
+            if sample:
+                m[2].record(s)
+                marks.append(m)
 
     # clock settle (untimed): steps for --settle-s seconds of wall time, checked every
     # few steps with a device sync; then the W warm-up steps
     t_settle, i_settle = time.perf_counter(), 0
     while time.perf_counter() - t_settle < args.settle_s:
         for _ in range(8):
-            run(i_settle)
+            run(i_settle, streams[i_settle % S], i_settle % S)
             i_settle += 1
         torch.cuda.synchronize(dev)
     settle_steps = i_settle
@@ -474,8 +493,12 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    for s in streams[1:]:
+        s.wait_event(ev0)
     for i in range(args.steps):
         step(args.warmup + i)
+    for s in streams[1:]:
+        stream.wait_stream(s)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -483,6 +506,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     exchange_ms = None
+    single_ms = None
     if world > 1:
         for i in range(max(4, args.steps // 4)):
             step(args.warmup + args.steps + i, sample=True)
@@ -491,6 +515,19 @@ def main():
         kernel_ms = sum(m[1].elapsed_time(m[2]) for m in marks) / len(marks)
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
+        if S > 1:
+            # the roofline is per kernel: its launch duration comes from max(4, K/4) more
+            # frames on ONE stream, back to back, after the timed region (the S-stream
+            # launches overlap, so their event spans are not launch durations)
+            n1 = max(4, args.steps // 4)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(n1):
+                run(args.warmup + args.steps + i)
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            single_ms = e0.elapsed_time(e1) / n1
+    launch_ms = single_ms if single_ms is not None else kernel_ms
     stage_ms = None
     fused = cfg["kind"] == "texture" and world == 1 and args.texture_mode == "fused"
     if cfg["kind"] == "texture" and world == 1 and not fused:
@@ -505,14 +542,14 @@ def main():
         nit = cfg["nitr"]
         guide = sum(m[2 * t].elapsed_time(m[2 * t + 1]) for m in smarks for t in range(nit))
         jbf = sum(m[2 * t + 1].elapsed_time(m[2 * t + 2]) for m in smarks for t in range(nit))
-        per = kernel_ms / nit
+        per = launch_ms / nit
         stage_ms = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
                     "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
-    t = torch.tensor([elapsed, kernel_ms, exchange_ms or 0.0], dtype=torch.float64,
+    t = torch.tensor([elapsed, launch_ms, exchange_ms or 0.0], dtype=torch.float64,
                      device=dev if args.backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
+    elapsed, launch_ms = float(t[0]), float(t[1])
     exchange_ms = float(t[2]) if world > 1 else None
 
     px_per_rank = rows * w
@@ -521,26 +558,26 @@ def main():
     value = total_px / (elapsed / args.steps) / 1e6
 
     if fused:
-        roof = texture_fused_roofline(cfg, px_per_rank, kernel_ms)
+        roof = texture_fused_roofline(cfg, px_per_rank, launch_ms)
     elif cfg["kind"] == "texture":
-        roof = texture_roofline(args.config, cfg, px_per_rank, kernel_ms, stage_ms)
+        roof = texture_roofline(args.config, cfg, px_per_rank, launch_ms, stage_ms)
     else:
         taps = circle_taps(r)
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
-        tflops = flops / (kernel_ms * 1e-3) / 1e12
-        hbm = 6.0 * px_per_rank / (kernel_ms * 1e-3) / 1e9
+        tflops = flops / (launch_ms * 1e-3) / 1e12
+        hbm = 6.0 * px_per_rank / (launch_ms * 1e-3) / 1e9
         # the committed PMC summaries are single-GPU whole-frame launches
         traffic, tsrc = (None, None) if world > 1 else pmc_traffic(args.config, [f"void vip::{cfg['kind']}_kernel<{r},"])
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
-                    kernel=f"{cfg['kind']}_kernel<R={r}>", avg_launch_ms=round(kernel_ms, 4),
+                    kernel=f"{cfg['kind']}_kernel<R={r}>", avg_launch_ms=round(launch_ms, 4),
                     flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
-                    gtaps_per_s=round(taps * px_per_rank / (kernel_ms * 1e-3) / 1e9, 1),
+                    gtaps_per_s=round(taps * px_per_rank / (launch_ms * 1e-3) / 1e9, 1),
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
                              bytes_per_px=6))
         if world == 1:  # the committed PMC summaries are whole-frame launches
-            roof["valu_issue"] = valu_issue(args.config, f"void vip::{cfg['kind']}_kernel<{r},", kernel_ms)
+            roof["valu_issue"] = valu_issue(args.config, f"void vip::{cfg['kind']}_kernel<{r},", launch_ms)
 
     out = {
         "metric": BASELINE_METRIC if args.config == "c2" else f"Mpixels/sec {cfg['workload']}",
@@ -561,9 +598,14 @@ def main():
                    **({"texture_mode": args.texture_mode} if cfg["kind"] == "texture" and world == 1 else {}),
                    **({"backend": args.backend} if world > 1 else {})},
         "roofline": roof,
-        # per step, max over ranks: the kernel(s) and, at N>1, the halo exchange before
-        # them (event-timed on the filter stream in max(4, K/4) steps after the timed region)
-        "kernel_ms": round(kernel_ms, 4),
+        # per step, max over ranks: the kernel(s) of one frame on one stream and, at N>1,
+        # the halo exchange before them (event-timed on the filter stream in max(4, K/4)
+        # steps after the timed region); the roofline's launch durations come from it
+        "kernel_ms": round(launch_ms, 4),
+        # frames in flight on S streams (step i on stream i % S); at N=1 and S>1 the
+        # timed region's device time per frame, all streams together
+        "streams": S,
+        **({"frame_ms_in_flight": round(kernel_ms, 4)} if world == 1 and S > 1 else {}),
         "settle": {"seconds": args.settle_s, "steps": settle_steps},
         **({"exchange_ms": round(exchange_ms, 4)} if exchange_ms is not None else {}),
     }
