@@ -157,6 +157,30 @@ __global__ __launch_bounds__(1024) void k(float* out, float a, float b) {
                 else asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
                 if (i == 7) asm volatile("s_waitcnt lgkmcnt(0)");
             }
+            if constexpr (KIND == 41) {  // f16 (lo half) x f32 + f32 -> f32
+                asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x[i]) : "v"(u[(i + 1) & 7]), "v"(a));
+            }
+            if constexpr (KIND == 42) {  // folded JBF tap on an f16 source plane: sad, min, lshl_or,
+                                         // 3 fma_mix, add (+ 1 fma_mix to make 8)
+                switch (i) {
+                    case 0: asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[0]) : "v"(u[1]), "v"(u[3])); break;
+                    case 1: asm volatile("v_min_u32 %0, %0, %1" : "+v"(u[2]) : "v"(u[5])); break;
+                    case 2: asm volatile("v_lshl_or_b32 %0, %0, 7, %1" : "+v"(u[4]) : "v"(u[5])); break;
+                    case 3: asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x[1]) : "v"(u[6]), "v"(a)); break;
+                    case 4: asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(x[2]) : "v"(u[6]), "v"(a)); break;
+                    case 5: asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x[3]) : "v"(u[7]), "v"(a)); break;
+                    case 6: asm volatile("v_add_f32 %0, %1, %0" : "+v"(x[4]) : "v"(a)); break;
+                    default: asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x[5]) : "v"(u[6]), "v"(a)); break;
+                }
+            }
+            if constexpr (KIND == 43) {  // fma_mix / fma 1:1
+                if (i & 1) asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
+                else asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x[i]) : "v"(u[(i + 1) & 7]), "v"(a));
+            }
+            if constexpr (KIND == 44) {  // fma_mix / sad 1:1
+                if (i & 1) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
+                else asm volatile("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[1,0,0]" : "+v"(x[i]) : "v"(u[(i + 1) & 7]), "v"(a));
+            }
             if constexpr (KIND == 35) {  // 1 slow : 3 fast
                 if ((i & 3) == 0) asm volatile("v_sad_u8 %0, %1, %2, %0" : "+v"(u[i]) : "v"(u[(i + 1) & 7]), "v"(u[(i + 3) & 7]));
                 else asm volatile("v_fma_f32 %0, %1, %2, %0" : "+v"(x[i]) : "v"(a), "v"(b));
@@ -229,5 +253,10 @@ int main() {
     run<38>("mix sad,lshl_or,2 pk_fma", d, blocks, 0);
     run<39>("mix pk_mul/mul 1:1", d, blocks, 0);
     run<40>("mix ds_read/fma 1:3", d, blocks, 0);
+    run<41>("v_fma_mix_f32", d, blocks, 0);
+    run<42>("mix folded f16 JBF tap 8", d, blocks, 0);
+    run<43>("mix fma_mix/fma 1:1", d, blocks, 0);
+    run<44>("mix fma_mix/sad 1:1", d, blocks, 0);
+    run<33>("mix bilateral pair 8", d, blocks, 0);
     return 0;
 }

@@ -489,3 +489,33 @@ def test_device_buffer_validation(dev):
     impl = _BilateralImpl(64, 32, 9)
     with pytest.raises(vip.VipError):  # C ABI: row range outside the handle's rows
         impl.run_rows(dev.empty((40, 64, 3)), good, 8, 0, 0, 40)
+
+
+@pytest.mark.parametrize("kind", ["bilateral", "adaptive", "texture"])
+def test_frames_in_flight_on_two_streams(dev, oracle, kind):
+    """bench.py's mode: frames i = 0..5 alternate over two HIP streams with no sync
+    between them (one handle per stream for the texture filter, which owns scratch
+    frames; one shared handle otherwise) -- every output equals the oracle."""
+    torch = dev.torch_
+    h, w = 360, 640
+    imgs = [np.random.default_rng(100 + i).integers(0, 255, (h, w, 3), dtype=np.uint8) for i in range(6)]
+    srcs = [dev.put(a) for a in imgs]
+    dsts = [dev.empty((h, w, 3)) for _ in imgs]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    if kind == "bilateral":
+        f = _BilateralImpl(w, h, 15)
+        hs = [lambda s, d, st: f.bilateral_filter(s, d, stream=st)] * 2
+        want = [oracle.bilateral(a, 15) for a in imgs]
+    elif kind == "adaptive":
+        f = _AdaptiveImpl(w, h, 15)
+        hs = [lambda s, d, st: f.execute(s, d, stream=st)] * 2
+        want = [oracle.adaptive(a, 15) for a in imgs]
+    else:
+        ts = [_TextureImpl(w, h, 5, 3) for _ in range(2)]
+        hs = [lambda s, d, st, t=t: t.execute(s, d, stream=st) for t in ts]
+        want = [oracle.texture(a, 5, 3) for a in imgs]
+    for i in range(6):
+        hs[i % 2](srcs[i], dsts[i], streams[i % 2])
+    for i in range(6):
+        got = dev.get(dsts[i])
+        assert np.array_equal(got, want[i]), f"frame {i}: " + _mismatch(got, want[i])
