@@ -114,7 +114,10 @@ int vip_gradient_f32(const float* d_src, float* d_dst, int width, int height, in
  *      (include/cuda/bilateral_texture_filter.hpp:7-17, src/bilateral_texture_filter_impl.cu:179-275) ---- */
 int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int nitr, int numerics);
 int vip_texture_destroy(vip_texture_t h);
-/* Impl::execute (:199-214); d_src and d_dst are dense width*3 */
+/* Impl::execute (:199-214); d_src and d_dst are dense width*3. The handle owns scratch
+ * frames (like the reference's Impl): runs on one handle must not overlap, so frames in
+ * flight on several streams take one handle per stream. Bilateral and adaptive handles
+ * hold only read-only LUTs and may run on several streams at once. */
 int vip_texture_run(vip_texture_t h, const uint8_t* d_src, uint8_t* d_dst, void* stream);
 /* vip_texture_run with per-stage timestamps (measurement; no reference counterpart):
  * `events` holds 2*nitr + 1 hipEvent_t (created with timing enabled, passed as void*);

@@ -658,6 +658,42 @@ VIP_GF_STAMP(8);
         const int tx = run % G::TW, ty0 = (run / G::TW) * kGfRun;
         const int x = x0 + tx;
         if (x > W1 || y0 + ty0 >= gy1) continue;
+#ifndef VIP_GF_ARGMIN_SCAN
+        // rtv is finite and >= +0 (num >= 0, msum + 1e-9 > 0), so its bit patterns order
+        // like its values: each row's minimum is an integer min3 (no NaN canonicalising),
+        // its first position the lowest column holding that minimum -- the same position
+        // as the reference's strict > scan. Every rtv is <= 255 < the scan's initial 1e10f
+        // (FLT_MAX in the CPP profile), so that initial value never survives.
+        uint32_t rv[kGfRun + 2 * R];
+        int ri[kGfRun + 2 * R];
+#pragma unroll
+        for (int t = 0; t < kGfRun + 2 * R; ++t) {  // window rows ty0-R .. ty0+kGfRun-1+R
+            const float* row = RR + (ty0 + t) * G::BW + tx;
+            uint32_t m[K];
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) m[kx] = __float_as_uint(row[kx]);
+            uint32_t v = m[0];
+#pragma unroll
+            for (int kx = 1; kx < K; ++kx) v = v < m[kx] ? v : m[kx];
+            int c = K - 1;
+#pragma unroll
+            for (int kx = K - 2; kx >= 0; --kx) c = m[kx] == v ? kx : c;
+            rv[t] = v;
+            ri[t] = (ty0 + t) * G::BW + tx + c;
+        }
+#pragma unroll
+        for (int j = 0; j < kGfRun; ++j) {
+            VIP_GF_PROGRESS(j * 4 / kGfRun);
+            const int y = y0 + ty0 + j;
+            if (y >= gy1) break;
+            uint32_t mb = rv[j];
+#pragma unroll
+            for (int ky = 1; ky < K; ++ky) mb = mb < rv[j + ky] ? mb : rv[j + ky];
+            int mi = ri[j + K - 1];
+#pragma unroll
+            for (int ky = K - 2; ky >= 0; --ky) mi = rv[j + ky] == mb ? ri[j + ky] : mi;
+            const float rmin = __uint_as_float(mb);
+#else  // the reference's scan: compare and select per position
         float rv[kGfRun + 2 * R];
         int ri[kGfRun + 2 * R];
 #pragma unroll
@@ -689,6 +725,7 @@ VIP_GF_STAMP(8);
                     mi = ri[j + ky];
                 }
             }
+#endif
             const int ci = (ty0 + j + R) * G::BW + tx + R;
             const float arg = sigma_alpha * (RR[ci] - rmin);
 #ifdef VIP_GF_ABL_EXP  // timing ablation only (inexact): hardware exp2
