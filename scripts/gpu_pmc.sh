@@ -14,7 +14,7 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_
            "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- python bench.py $ARGS --steps 5 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc $set -d $OUT/p$i -o run --output-format csv -- python bench.py $ARGS --streams 1 --steps 5 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
   rc=$?; echo "pmc pass $i rc=$rc"
   [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit $rc; }
 done

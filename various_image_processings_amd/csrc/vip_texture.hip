@@ -534,7 +534,9 @@ VIP_GF_STAMP(8);
         if (ix >= 0 && ix <= W1 && iy0 >= H0 && iy0 + kGfV2 - 1 <= H1) {
             constexpr int NV = kGfV2 + K - 1;
             uint32_t hrb[NV], hg[NV], hmx[NV];
-            float rowmax[NV];
+            // magnitudes are finite and >= +0: their bit patterns order like their values, so
+            // the extremes are integer max3s (no NaN canonicalising of LDS loads)
+            uint32_t rowmax[NV], mmaxb[kGfV2];
 #pragma unroll
             for (int t = 0; t < NV; ++t) {
                 hrb[t] = H[(p0 + t) * G::HWP + c];
@@ -562,9 +564,12 @@ VIP_GF_STAMP(8);
                 float m[K];
 #pragma unroll
                 for (int kx = 0; kx < K; ++kx) m[kx] = mrow[kx];
-                float mx = m[0];
+                uint32_t mx = __float_as_uint(m[0]);
 #pragma unroll
-                for (int kx = 1; kx < K; ++kx) mx = __builtin_fmaxf(mx, m[kx]);  // == the reference's max (no NaN)
+                for (int kx = 1; kx < K; ++kx) {  // == the reference's max (no NaN)
+                    const uint32_t b = __float_as_uint(m[kx]);
+                    mx = mx > b ? mx : b;
+                }
                 rowmax[t] = mx;
                 // window row t - j of output j, in the reference's row-major order
 #pragma unroll
@@ -576,7 +581,9 @@ VIP_GF_STAMP(8);
                     for (int kx = 1; kx < K; ++kx) msum[j] = msum[j] + m[kx];
                 }
             }
-            win_op<kGfV2, K>(rowmax, mmax, [](float a, float b) { return __builtin_fmaxf(a, b); });
+            win_op<kGfV2, K>(rowmax, mmaxb, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+#pragma unroll
+            for (int j = 0; j < kGfV2; ++j) mmax[j] = __uint_as_float(mmaxb[j]);
         } else {
             // a centre outside the image: the reference reads the stage values at the
             // clamped centre, whose window lies inside the pre-clamped regions
