@@ -12,5 +12,8 @@ hipcc $F -DVIP_ONLY_R7 -c vip_bilateral.hip -o /tmp/var_$name/bm.o
 hipcc $F -DVIP_ONLY_R7 -DVIP_BIL_JOINT -c vip_bilateral.hip -o /tmp/var_$name/bjm.o
 hipcc $F -DVIP_ONLY_R7 -DVIP_ADA_FMA -c vip_adaptive.hip -o /tmp/var_$name/a.o
 hipcc $F -DVIP_ONLY_R7 -c vip_adaptive.hip -o /tmp/var_$name/am.o
-hipcc --offload-arch=gfx950 -shared -o ../../variants/$name.so /tmp/var_$name/*.o build/vip_texture.o build/vip_capi.o build/vip_cuda_api.o
+# the texture, C ABI and C++ API objects of the in-place CMake build (__graft_entry__.build())
+O=../../build/cmake/CMakeFiles
+hipcc --offload-arch=gfx950 -shared -o ../../variants/$name.so /tmp/var_$name/*.o \
+  $(ls $O/vip_{texture,capi}.dir/various_image_processings_amd/csrc/*.o $O/vip_hip.dir/various_image_processings_amd/csrc/*.o)
 echo built variants/$name.so

@@ -366,8 +366,13 @@ __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t*
         const uint32_t p = row.source(j - 4 * C0);
         const int b = (j - J0) % NB;
         n01[b].x = (float)(p & 0xffu);
+#ifdef VIP_ABL_CVT  // timing ablation only (wrong output): one byte conversion per column
+        n01[b].y = n01[b].x;
+        n21[b].x = n01[b].x;
+#else
         n01[b].y = (float)((p >> 8) & 0xffu);
         n21[b].x = (float)((p >> 16) & 0xffu);
+#endif
         n21[b].y = 1.0f;
 #pragma unroll
         for (int i = 0; i < P; ++i) {
