@@ -47,3 +47,35 @@ def test_committed_bench_lines_carry_the_contract_fields():
         roof = line["roofline"]
         assert roof["frac"] == pytest.approx(roof["achieved"] / roof["peak"], rel=1e-2)
         assert line["cpu_baseline"]["kind"] in ("port", "reference")
+
+
+def test_kernel_busy_isolated_and_union(tmp_path):
+    """scripts/kernel_busy.py: launches that overlap another are not 'isolated', and the
+    busy time is the union of the launch intervals (frames in flight on two streams)."""
+    import subprocess
+    rows = [("k", 0, 100), ("k", 50, 150), ("k", 200, 300), ("j", 310, 330)]
+    f = tmp_path / "run_kernel_trace.csv"
+    f.write_text("Kernel_Name,Start_Timestamp,End_Timestamp\n" + "".join(f"{n},{s},{e}\n" for n, s, e in rows))
+    out = tmp_path / "busy.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "kernel_busy.py"), str(f), str(out)], check=True,
+                   capture_output=True)
+    d = json.loads(out.read_text())
+    assert d["launches"] == 4
+    assert d["busy_ns_per_launch"] == (150 + 100 + 20) / 4
+    assert d["kernels"]["k"]["launches"] == 3 and d["kernels"]["k"]["isolated_launches"] == 1
+    assert d["kernels"]["k"]["isolated_mean_us"] == 0.1
+    assert d["kernels"]["j"]["isolated_launches"] == 1
+
+
+def test_committed_lines_time_the_roofline_on_one_stream():
+    """With frames in flight (streams > 1) the roofline's launch duration is the single-
+    stream one, which the committed rocprofv3 isolated launches must agree with (<= 3 %)."""
+    for cfg, kern in (("c2", "void vip::bilateral_kernel<7,"), ("c4", "void vip::texture_guide_fused_kernel<2,")):
+        line = json.load(open(os.path.join(ROOT, "profiles", f"r02_{cfg}_bench.json")))
+        busy = json.load(open(os.path.join(ROOT, "profiles", f"r02_{cfg}_busy.json")))
+        assert line["streams"] == 2 and line["frame_ms_in_flight"] <= line["kernel_ms"]
+        iso = [v["isolated_mean_us"] for n, v in busy["kernels"].items() if n.startswith(kern)][0]
+        r = line["roofline"]
+        launch_ms = r["avg_launch_ms"] if cfg == "c2" else \
+            [k["avg_launch_ms"] for k in (r["dominant"], r["other"]) if "guide" in k["kernel"]][0]
+        assert abs(iso / 1e3 - launch_ms) / launch_ms < 0.03, (cfg, iso, launch_ms)
