@@ -396,6 +396,7 @@ def main():
     # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     stream = streams[0]
+    sraw = [st.cuda_stream for st in streams]  # hipStream_t of each stream
     w = cfg["width"]
     k = cfg["ksize"]
     r = k // 2
@@ -415,8 +416,10 @@ def main():
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         smarks = []
 
-        def run(i, s=stream, h=0):
-            texs[h].execute(srcs[i % NBUF], dsts[i % NBUF], stream=s)
+        sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
+
+        def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
+            texs[h].execute(sp[i % NBUF], dp[i % NBUF], stream=sraw[h])
 
         def run_staged(i):
             """one frame with per-stage events (vip_texture_run_timed)"""
@@ -445,8 +448,10 @@ def main():
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
 
-        def run(i, s=stream, h=0):
-            sb.filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
+        sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
+
+        def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
+            sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h], exchange=False)
 
     # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time per frame
     # (with S > 1 streams: per frame with S frames in flight).
