@@ -8,6 +8,8 @@
 //     float midpoints' neighbourhoods -- Markstein's theorem makes (b) follow from (a),
 //     this is the empirical cross-check.
 // (c) vip::sqrt_int_exact against sqrtf for every integer in [0, 2^20) (texture gradient).
+// (d) vip::pack_u8_clamped against clampi((int)v, 0, 255) for every float |v| < 2048 (the
+//     texture guide's blend: v in [-255, 511]).
 // Exit status 0 iff no mismatch against the IEEE divide / sqrt (hipcc default, correctly
 // rounded). Run on the GPU: tests/test_gpu_parity.py::test_epilogue_division_exact.
 #include <hip/hip_runtime.h>
@@ -17,7 +19,19 @@
 
 #include "vip_stencil.hpp"
 
-__device__ unsigned long long g_bad[3];
+__device__ unsigned long long g_bad[4];
+
+// (d) every float with |v| < 2048: both signs of the bit patterns [0, 0x45000000)
+__global__ void pack_u8_all(uint32_t n) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+#pragma unroll
+    for (uint32_t sign = 0; sign < 2; ++sign) {
+        const float v = __uint_as_float((sign << 31) | i);
+        const uint32_t want = (uint32_t)vip::clampi((int)v, 0, 255) << 16 | 0xa5005aa5u;  // byte 2 replaced
+        if (vip::pack_u8_clamped(v, 2, 0xa5a55aa5u) != want) atomicAdd(&g_bad[3], 1ull);
+    }
+}
 
 // (c) the texture gradient's integer square root: vip::sqrt_int_exact == sqrtf (hipcc's
 //     correctly rounded expansion) for every integer in [0, n)
@@ -62,7 +76,7 @@ __global__ void quot_random(uint64_t base) {
 }
 
 int main() {
-    unsigned long long zero[3] = {0, 0, 0};
+    unsigned long long zero[4] = {0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero)) != hipSuccess) return 2;
     // bit patterns of 1.0f and 2^17: the epilogue's sums of weights lie in [1, 1024), the
     // texture guide's 1 + exp(x) in [2, 2^17)
@@ -74,10 +88,13 @@ int main() {
         hipLaunchKernelGGL(quot_random, dim3((unsigned)(per / 256)), dim3(256), 0, 0, rep * per);
     const uint32_t nsq = 1u << 20;
     hipLaunchKernelGGL(sqrt_ints, dim3(nsq / 256), dim3(256), 0, 0, nsq);
-    unsigned long long bad[3];
+    const uint32_t npk = 0x45000000u;
+    hipLaunchKernelGGL(pack_u8_all, dim3((npk + 255) / 256), dim3(256), 0, 0, npk);
+    unsigned long long bad[4];
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
     std::printf("reciprocal: %u floats k in [1, 2^17), %llu mismatches\n", n, bad[0]);
     std::printf("quotient: %llu random (s, k), %llu mismatches\n", (unsigned long long)(16 * per), bad[1]);
     std::printf("integer sqrt: %u integers in [0, 2^20), %llu mismatches\n", nsq, bad[2]);
-    return (bad[0] || bad[1] || bad[2]) ? 1 : 0;
+    std::printf("u8 clamp pack: %u floats |v| < 2048 of each sign, %llu mismatches\n", npk, bad[3]);
+    return (bad[0] || bad[1] || bad[2] || bad[3]) ? 1 : 0;
 }

@@ -433,15 +433,16 @@ def test_texture_iterate_rows_band(dev, oracle):
 def test_epilogue_division_exact():
     """The bilateral/joint epilogue divides by sumk via one reciprocal (vip_stencil.hpp
     recip_exact/div_by_sumk). microbench/div_check checks RN(1/k) for EVERY float k in
-    [1, 1024) and 2^30 quotients against the IEEE divide on the GPU, and the texture
-    gradient's sqrt_int_exact against sqrtf for every integer in [0, 2^20)."""
+    [1, 1024) and 2^30 quotients against the IEEE divide on the GPU, the texture
+    gradient's sqrt_int_exact against sqrtf for every integer in [0, 2^20), and the guide
+    blend's pack_u8_clamped against the clamp for every float |v| < 2048."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(__file__), "..", "microbench", "div_check")
     assert os.path.exists(exe), "build first: make -C various_image_processings_amd/csrc"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(" 0 mismatches") == 3, r.stdout
+    assert r.stdout.count(" 0 mismatches") == 4, r.stdout
 
 
 @pytest.mark.parametrize("k,ss,sc", [(31, 1000.0, 1000.0), (5, 0.1, 0.1), (15, 3.0, 1e4), (7, 1e4, 0.5)])

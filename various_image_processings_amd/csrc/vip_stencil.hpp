@@ -431,6 +431,14 @@ __device__ __forceinline__ float sqrt_int_exact(float x) {
     return __builtin_fmaf(-sp, s, x) > 0.f ? sp : s1;
 }
 
+// clampi((int)v, 0, 255) written into byte `sel` of `word`: floor (the int conversion's
+// truncation for v >= 0, and below 0 either way) then v_cvt_pk_u8_f32, whose float->u8
+// conversion saturates (an integral input, so its rounding is moot) and packs in the same
+// instruction. microbench/div_check compares it with the clamp for every float |v| < 2048.
+__device__ __forceinline__ uint32_t pack_u8_clamped(float v, uint32_t sel, uint32_t word) {
+    return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_floorf(v), sel, word);
+}
+
 // RN(1/k) for k in [1, 2^17): hardware rcp (1 ulp) + one Newton step. Verified
 // exhaustively over every float of that range by microbench/div_check.hip.
 __device__ __forceinline__ float recip_exact(float k) {

@@ -749,7 +749,7 @@ VIP_GF_STAMP(8);
             for (int c = 0; c < 3; ++c) {
                 const float bm = BR[c * G::BPL + mi], bc = BR[c * G::BPL + ci];
                 const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
-                gw |= (uint32_t)clampi((int)v, 0, 255) << (8 * c);
+                gw = pack_u8_clamped(v, c, gw);  // == clampi((int)v, 0, 255) << 8c
             }
             sink(ty0 + j, tx, gw);
         }
