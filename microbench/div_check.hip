@@ -10,6 +10,8 @@
 // (c) vip::sqrt_int_exact against sqrtf for every integer in [0, 2^20) (texture gradient).
 // (d) vip::pack_u8_clamped against clampi((int)v, 0, 255) for every float |v| < 2048 (the
 //     texture guide's blend: v in [-255, 511]).
+// (e) vip::exp_tab_f32 against (float)exp((double)x) (ocml's double exp) for every float x
+//     in [0, 32) (the texture guide's alpha argument lies in [0, 25.5]).
 // Exit status 0 iff no mismatch against the IEEE divide / sqrt (hipcc default, correctly
 // rounded). Run on the GPU: tests/test_gpu_parity.py::test_epilogue_division_exact.
 #include <hip/hip_runtime.h>
@@ -19,7 +21,22 @@
 
 #include "vip_stencil.hpp"
 
-__device__ unsigned long long g_bad[4];
+__device__ unsigned long long g_bad[5];
+__device__ unsigned int g_exp_bad_x[16];
+
+__global__ void exp_all(uint32_t n) {
+    __shared__ double etab[64];
+    if (threadIdx.x < 64) etab[threadIdx.x] = vip::kExp2Tab64[threadIdx.x];
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = __uint_as_float(i);
+    const float want = (float)exp((double)x);
+    if (__float_as_uint(vip::exp_tab_f32(x, etab)) != __float_as_uint(want)) {
+        const unsigned long long slot = atomicAdd(&g_bad[4], 1ull);
+        if (slot < 16) g_exp_bad_x[slot] = i;
+    }
+}
 
 // (d) every float with |v| < 2048: both signs of the bit patterns [0, 0x45000000)
 __global__ void pack_u8_all(uint32_t n) {
@@ -76,7 +93,7 @@ __global__ void quot_random(uint64_t base) {
 }
 
 int main() {
-    unsigned long long zero[4] = {0, 0, 0, 0};
+    unsigned long long zero[5] = {0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero)) != hipSuccess) return 2;
     // bit patterns of 1.0f and 2^17: the epilogue's sums of weights lie in [1, 1024), the
     // texture guide's 1 + exp(x) in [2, 2^17)
@@ -90,11 +107,19 @@ int main() {
     hipLaunchKernelGGL(sqrt_ints, dim3(nsq / 256), dim3(256), 0, 0, nsq);
     const uint32_t npk = 0x45000000u;
     hipLaunchKernelGGL(pack_u8_all, dim3((npk + 255) / 256), dim3(256), 0, 0, npk);
-    unsigned long long bad[4];
+    const uint32_t nexp = 0x42000000u;  // bit patterns of [0, 32)
+    hipLaunchKernelGGL(exp_all, dim3((nexp + 255) / 256), dim3(256), 0, 0, nexp);
+    unsigned long long bad[5];
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
     std::printf("reciprocal: %u floats k in [1, 2^17), %llu mismatches\n", n, bad[0]);
     std::printf("quotient: %llu random (s, k), %llu mismatches\n", (unsigned long long)(16 * per), bad[1]);
     std::printf("integer sqrt: %u integers in [0, 2^20), %llu mismatches\n", nsq, bad[2]);
     std::printf("u8 clamp pack: %u floats |v| < 2048 of each sign, %llu mismatches\n", npk, bad[3]);
-    return (bad[0] || bad[1] || bad[2] || bad[3]) ? 1 : 0;
+    std::printf("exp: %u floats x in [0, 32), %llu mismatches\n", nexp, bad[4]);
+    if (bad[4]) {
+        unsigned int xs[16];
+        if (hipMemcpyFromSymbol(xs, HIP_SYMBOL(g_exp_bad_x), sizeof(xs)) == hipSuccess)
+            for (unsigned long long j = 0; j < bad[4] && j < 16; ++j) std::printf("  exp mismatch at x = %a\n", (double)__builtin_bit_cast(float, xs[j]));
+    }
+    return (bad[0] || bad[1] || bad[2] || bad[3] || bad[4]) ? 1 : 0;
 }

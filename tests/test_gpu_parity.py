@@ -442,7 +442,7 @@ def test_epilogue_division_exact():
     assert os.path.exists(exe), "build first: make -C various_image_processings_amd/csrc"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(" 0 mismatches") == 4, r.stdout
+    assert r.stdout.count(" 0 mismatches") == 5, r.stdout
 
 
 @pytest.mark.parametrize("k,ss,sc", [(31, 1000.0, 1000.0), (5, 0.1, 0.1), (15, 3.0, 1e4), (7, 1e4, 0.5)])

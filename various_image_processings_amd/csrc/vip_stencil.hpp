@@ -431,6 +431,32 @@ __device__ __forceinline__ float sqrt_int_exact(float x) {
     return __builtin_fmaf(-sp, s, x) > 0.f ? sp : s1;
 }
 
+// 2^(j/64), j = 0..63, correctly rounded to double (staged into LDS by the kernels that
+// call exp_tab_f32; internal linkage, one copy per translation unit).
+static __constant__ double kExp2Tab64[64] = {
+#include "vip_exp_tab64.inc"
+};
+
+// (float)exp((double)x) for float x in [0, 32) -- the texture guide's alpha argument
+// sigma_alpha * (rtv - rtv_min) lies in [0, 255 / (5 ksize)] -- in 14 double ops:
+// x = (k/64) ln2 + r with |r| <= ln2/128 (two-part Cody-Waite; k < 2^12, so k * HI is
+// exact), exp(r) - 1 by its degree-5 Taylor polynomial (truncation < 2^-54), times
+// 2^(k mod 64 / 64) from `etab` (kExp2Tab64 in LDS) and 2^(k / 64). microbench/div_check
+// compares it with (float)exp((double)x) for EVERY float in [0, 32).
+__device__ __forceinline__ float exp_tab_f32(float xf, const double* etab) {
+    const double x = (double)xf;
+    const double kd = __builtin_rint(x * 0x1.71547652b82fep+6);  // 64 / ln2
+    const int k = (int)kd;
+    double r = __builtin_fma(-kd, 0x1.62e42fefa3000p-7, x);       // ln2/64, 12 low bits clear
+    r = __builtin_fma(-kd, 0x1.3de6af278ece6p-48, r);             // ln2/64 - HI
+    double q = __builtin_fma(r, 1.0 / 120, 1.0 / 24);
+    q = __builtin_fma(r, q, 1.0 / 6);
+    q = __builtin_fma(r, q, 0.5);
+    const double p = __builtin_fma(r * r, q, r);                  // exp(r) - 1
+    const double t = etab[k & 63];
+    return (float)__builtin_ldexp(__builtin_fma(t, p, t), k >> 6);
+}
+
 // clampi((int)v, 0, 255) written into byte `sel` of `word`: floor (the int conversion's
 // truncation for v >= 0, and below 0 either way) then v_cvt_pk_u8_f32, whose float->u8
 // conversion saturates (an integral input, so its rounding is moot) and packs in the same

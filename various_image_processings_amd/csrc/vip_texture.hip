@@ -301,6 +301,9 @@ struct GfGeomT {
     // H after it (RB, MX words + G as u16); BR/RR and the guide tile GT reuse it all
     static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL + TW * TH);
     static constexpr int WORDS = A_WORDS;
+    // the exp table (64 doubles) after every region, read by the guide phase
+    static constexpr int ETAB = round_up(WORDS, 4);
+    static constexpr int WORDS_ALL = ETAB + 128;
     static_assert(MW * MH <= XR_WORDS, "MR reuses the XR region");
     static constexpr int NR1 = HH * (HWP / kGfH1);      // pass-1 runs
     static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
@@ -384,6 +387,7 @@ __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restr
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
     float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
+    double* const etab = reinterpret_cast<double*>(lds + G::ETAB);  // kExp2Tab64
     // OPAQUE_TID (the fused iteration kernel, which calls this three times): without it
     // the compiler keeps chunk 0's thread-index arithmetic live across the later chunks
     // (18 spilled VGPRs, ~90 MB of scratch writes per 4K launch); recomputing is cheaper.
@@ -433,6 +437,9 @@ __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restr
             }
         }
 VIP_GF_STAMP(8);
+#ifndef VIP_GF_EXP_OCML
+        if (tid < 64) etab[tid] = kExp2Tab64[tid];  // read in phase 4, after several barriers
+#endif
 #pragma unroll
         for (int k = 0; k < KG; ++k) {
             const int g = tid + k * G::NT;
@@ -737,8 +744,12 @@ VIP_GF_STAMP(8);
             const float arg = sigma_alpha * (RR[ci] - rmin);
 #ifdef VIP_GF_ABL_EXP  // timing ablation only (inexact): hardware exp2
             const float e = __builtin_amdgcn_exp2f(arg * 1.44269504f);
-#else
+#elif defined(VIP_GF_EXP_OCML)  // ocml's double exp
             const float e = (float)exp((double)arg);
+#else
+            // == (float)exp((double)arg) for every float arg in [0, 32) (microbench/div_check
+            // on the GPU; microbench/exp_check against glibc, the oracle's exp)
+            const float e = exp_tab_f32(arg, etab);
 #endif
             // 2 / (1 + e) == 2 * RN(1 / (1 + e)) exactly (a power-of-two scale); e >= 1, so
             // recip_exact's argument is in [2, 2^17) here, where div_check verifies it
@@ -804,7 +815,7 @@ template <int R, bool CPP>
 static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1, int ksize,
                      int aligned, hipStream_t stream) {
     using G = GfGeom<R>;
-    constexpr int LDS = 4 * G::WORDS;
+    constexpr int LDS = 4 * G::WORDS_ALL;
     static_assert(LDS <= kLdsBudget, "fused guide tile does not fit LDS");
     auto kern = texture_guide_fused_kernel<R, CPP>;
     static std::atomic<unsigned long long> attr_devs{0};
@@ -868,7 +879,7 @@ using FuJG = Geom<kFuJR, kFuP>;                // TW 128, L 4, S 140
 using FuGG = GfGeomT<kFuR, FuJG::TW + 2 * kFuJR, kFuChunk, kFuNT>;
 constexpr int kFuPlane = kFuRows * FuJG::S;
 constexpr int kFuLutWords = 768 * kFuCopies;
-constexpr int kFuScratch = cmax(FuGG::WORDS, kFuPlane + kFuLutWords);
+constexpr int kFuScratch = cmax(FuGG::WORDS_ALL, kFuPlane + kFuLutWords);
 constexpr int kFuLds = 4 * (kFuPlane + kFuScratch);
 static_assert(FuJG::L == kFuJR && FuGG::TW == FuJG::TW + 2 * FuJG::L, "guide chunk covers the plane columns");
 static_assert(kFuRows % kFuChunk == 0 && FuJG::S >= FuGG::TW, "plane geometry");
