@@ -238,3 +238,18 @@ def test_texture_rows_band_equals_full_frame(oracle):
     full = oracle.texture(img, 5, 3)
     for r0, n in ((0, 7), (50, 11), (131, 9)):
         assert np.array_equal(oracle.texture_rows(img, r0, n, 5, 3), full[r0:r0 + n])
+
+
+def test_table_exp_equals_glibc_exp(tmp_path):
+    """The texture guide's alpha uses a 64-entry-table double exp on the GPU
+    (vip_stencil.hpp exp_tab_f32); microbench/exp_check restates it bit for bit (same table,
+    constants and fma sequence) and compares it with glibc's (float)exp((double)x) -- the
+    oracle's -- for EVERY float x in [0, 32), the whole range the argument can take.
+    (div_check compares the device version with ocml's on the GPU.)"""
+    import subprocess
+    exe = tmp_path / "exp_check"
+    src = os.path.join(ROOT, "microbench", "exp_check.c")
+    inc = os.path.join(ROOT, "various_image_processings_amd", "csrc")
+    subprocess.run(["cc", "-O2", "-ffp-contract=off", "-I", inc, "-o", str(exe), src, "-lm", "-lpthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout + r.stderr
