@@ -70,11 +70,13 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
 
     int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x
     TilePrefetch<R, ROWS, NT, P> pf;
+    LutStage<NT, NE, COPIES> ls;  // LUT reads go out before the first tile's
+    ls.load(a.color);
     {
         const int mt = xcd_tile(tile, a.tiles_total);
         pf.issue(a.src, a.src_pitch, a, (mt % a.tiles_x) * G::TW, (mt / a.tiles_x) * TH);
     }
-    stage_lut<NT, NE, COPIES>(lut, a.color);
+    ls.store(lut);
     pf.commit(plane);
     __syncthreads();
 

@@ -94,16 +94,15 @@ __global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs
     // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
     int tile = blockIdx.x;
     TilePrefetch<R, ROWS, NT, P> pg, ps;
+    LutStage<NT, NTAB * NE, COPIES> ls;  // once per workgroup; its reads go out first
+    ls.load(FOLD ? a.fold : a.color);
     {
         const int mt = xcd_tile(tile, a.tiles_total);
         const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
         pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
-    if constexpr (FOLD)
-        stage_lut<NT, NTAB * NE, COPIES>(lut, a.fold);  // once per workgroup
-    else
-        stage_lut<NT, NE, COPIES>(lut, a.color);
+    ls.store(lut);
     pg.commit(gplane);
     if constexpr (JOINT) ps.commit(splane);
     __syncthreads();
@@ -213,6 +212,38 @@ constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
 #define VIP_JBF_SHORT_LUT 0
 #endif
 
+// Small frames (plain filter, R <= VIP_BIL_SMALL_MAX_R): a frame with fewer 128 x 64
+// tiles than CUs leaves CUs idle (C1's 512 x 512 lenna: 32 tiles on 256 CUs). The
+// same kernel on 8 or 4 waves has 128 x 32 / 128 x 16 tiles, so more CUs work, each
+// with fewer waves per SIMD. Chosen per launch by a per-CU time model:
+// rounds(W) * W * cost(W), cost = the per-wave slowdown at W/4 waves per SIMD
+// (measured); VIP_BIL_WAVES=16|8|4 forces one (measurement knob).
+#ifndef VIP_BIL_SMALL_MAX_R
+#define VIP_BIL_SMALL_MAX_R 8
+#endif
+inline int small_frame_waves(int tiles_x, int out_rows) {
+    static const int forced = [] {
+        const char* e = getenv("VIP_BIL_WAVES");
+        const int w = e ? atoi(e) : 0;
+        return (w == 16 || w == 8 || w == 4) ? w : 0;
+    }();
+    if (forced) return forced;
+    const int cus = device_cus();
+    const int cand[3] = {16, 8, 4};
+    const float cost[3] = {1.0f, 1.25f, 1.8f};
+    int best = 16;
+    float best_t = 0.f;
+    for (int i = 0; i < 3; ++i) {
+        const long long tiles = (long long)tiles_x * ((out_rows + cand[i] * 4 - 1) / (cand[i] * 4));
+        const float t = (float)((tiles + cus - 1) / cus) * cand[i] * cost[i];
+        if (i == 0 || t < best_t) best = cand[i], best_t = t;
+    }
+    return best;
+}
+
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES>
+static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream);
+
 template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false>
 static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
@@ -221,6 +252,20 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
+    if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
+        const int w = small_frame_waves((a.width + Geom<R, P>::TW - 1) / Geom<R, P>::TW, a.out_rows);
+        if (w == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8>(a, stream);
+        if (w == 4) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4>(a, stream);
+    }
+    return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, WAVES>(a, stream);
+}
+
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES>
+static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
+    constexpr int PLANES = JOINT ? 2 : 1;
+    constexpr int P = outputs_per_thread<R, PLANES>();
+    constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
+    constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int TH = WAVES * 4;
     constexpr int LDS = lds_bytes<R, WAVES, PLANES, LUTW, P>();
     auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD>;

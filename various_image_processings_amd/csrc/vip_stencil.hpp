@@ -50,7 +50,7 @@ struct StencilArgs {
 
 // One workgroup per CU of the current device (the 96 KiB LUT fills most of the CU's
 // LDS), each striding over tiles; fewer blocks than CUs when the frame has fewer tiles.
-inline int persistent_blocks(int tiles) {
+inline int device_cus() {
     static std::atomic<int> cus_by_dev[64];  // CU count per device, 0 = not queried yet
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) dev = 0;
@@ -60,6 +60,11 @@ inline int persistent_blocks(int tiles) {
             cus = 256;
         cus_by_dev[dev & 63].store(cus, std::memory_order_relaxed);
     }
+    return cus;
+}
+
+inline int persistent_blocks(int tiles) {
+    const int cus = device_cus();
     return tiles < cus ? tiles : cus;
 }
 
@@ -249,14 +254,40 @@ struct TilePrefetch {
 // Fill the interleaved colour LUT: word d*COPIES + c = color[d], for
 // 768 entries x 32 copies (bilateral, 96 KiB), 768 x 16 (joint bilateral when the
 // halved LUT buys more waves, 48 KiB) or 1536 x 16 (adaptive, 96 KiB).
+// load() issues all of a thread's LUT reads at once (a compile-time count), store()
+// writes them: a kernel calls load() before its first tile's HBM reads, so the LUT
+// words arrive during one round trip instead of one dependent L2 round trip per store
+// (the earlier runtime loop waited on vmcnt(0) -- the tile prefetch included -- at each
+// of its 6 iterations).
+template <int NT, int ENTRIES, int COPIES>
+struct LutStage {
+    static_assert(COPIES == 16 || COPIES == 32, "copies");
+    static constexpr int SHIFT = COPIES == 32 ? 3 : 2;  // log2(COPIES / 4 words per store)
+    static constexpr int N = ENTRIES * COPIES / 4;        // uint4 stores
+    static constexpr int K = (N + NT - 1) / NT;
+    uint32_t v[K];
+
+    __device__ __forceinline__ void load(const float* color) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int q = (int)threadIdx.x + k * NT;
+            if (N % NT == 0 || q < N) v[k] = __float_as_uint(color[q >> SHIFT]);
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t* lut) const {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int q = (int)threadIdx.x + k * NT;
+            if (N % NT == 0 || q < N) *reinterpret_cast<uint4*>(lut + 4 * q) = make_uint4(v[k], v[k], v[k], v[k]);
+        }
+    }
+};
+
 template <int NT, int ENTRIES, int COPIES>
 __device__ __forceinline__ void stage_lut(uint32_t* lut, const float* color) {
-    static_assert(COPIES == 16 || COPIES == 32, "copies");
-    constexpr int SHIFT = COPIES == 32 ? 3 : 2;  // log2(COPIES / 4 words per store)
-    for (int q = threadIdx.x; q < ENTRIES * COPIES / 4; q += NT) {
-        const uint32_t v = __float_as_uint(color[q >> SHIFT]);
-        *reinterpret_cast<uint4*>(lut + 4 * q) = make_uint4(v, v, v, v);
-    }
+    LutStage<NT, ENTRIES, COPIES> s;
+    s.load(color);
+    s.store(lut);
 }
 
 // Neighbour words of one tile row, columns [4*C0, 4*C0 + 4*NC), read from LDS in

@@ -923,8 +923,10 @@ __global__ __launch_bounds__(kFuNT) void texture_iteration_fused_kernel(const St
     //    colour LUT into the dead chunk scratch
     {
         TilePrefetch<JR, kFuRows, kFuNT, P> ps;
+        LutStage<kFuNT, 768, kFuCopies> ls;
+        ls.load(a.color);
         ps.issue(a.src, a.src_pitch, a, tx0, ty0);
-        stage_lut<kFuNT, 768, kFuCopies>(lut, a.color);
+        ls.store(lut);
         ps.commit(splane);
     }
     __syncthreads();
