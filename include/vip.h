@@ -93,6 +93,12 @@ int vip_joint_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_
 int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, const uint8_t* d_guide,
                            size_t guide_pitch, uint8_t* d_dst, size_t dst_pitch, int out_rows, int src_row0,
                            int row_lo, int row_hi, void* stream);
+/* Tuning knob, process-wide (no reference counterpart): waves per workgroup of the plain
+ * bilateral kernel for radius <= 8. 0 (default) = chosen per launch from the frame's
+ * tile count (small frames take 8 or 4 waves and smaller tiles so more CUs work);
+ * 16, 8 or 4 forces one. Results are identical for every setting (only the tiling
+ * changes). The environment variable VIP_BIL_WAVES sets the initial value. */
+int vip_bilateral_set_waves(int waves);
 
 /* ---- adaptive bilateral: CudaAdaptiveBilateralFilter
  *      (include/cuda/adaptive_bilateral_filter.hpp:9-19, src/adaptive_bilateral_filter_impl.cu:117-191) ---- */

@@ -62,6 +62,28 @@ def test_bilateral_large_frame(dev, oracle, k, ss, sc):
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
+# Small frames run the plain kernel on 8 or 4 waves with 128x32 / 128x16 tiles
+# (vip_bilateral_set_waves, radius <= 8). Every forced wave count must give the oracle's
+# bytes; 1300x400 has 275 tiles at 4 waves, so some workgroups take two.
+@pytest.mark.parametrize("waves", [16, 8, 4])
+@pytest.mark.parametrize("k", [3, 11, 17])
+def test_bilateral_forced_waves(dev, oracle, waves, k):
+    img = oracle.random_image(1300, 400)
+    vip.set_bilateral_waves(waves)
+    try:
+        got = _bilateral_gpu(dev, img, k)
+    finally:
+        vip.set_bilateral_waves(0)
+    want = oracle.bilateral(img, k, threads=16)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+def test_bilateral_set_waves_rejects_other_counts():
+    with pytest.raises(vip.VipError):
+        vip.set_bilateral_waves(12)
+    vip.set_bilateral_waves(0)
+
+
 @pytest.mark.parametrize("k", [3, 9, 15, 25, 31])
 @pytest.mark.parametrize("numerics,profile", PROFILES)
 def test_joint_bilateral(dev, oracle, k, numerics, profile):

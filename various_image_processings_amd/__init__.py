@@ -15,6 +15,7 @@ from .filters import (  # noqa: F401
     DeviceImage,
     cuda_gradient,
     device_synchronize,
+    set_bilateral_waves,
 )
 
 __version__ = "0.1.0"

@@ -217,16 +217,12 @@ constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
 // same kernel on 8 or 4 waves has 128 x 32 / 128 x 16 tiles, so more CUs work, each
 // with fewer waves per SIMD. Chosen per launch by a per-CU time model:
 // rounds(W) * W * cost(W), cost = the per-wave slowdown at W/4 waves per SIMD
-// (measured); VIP_BIL_WAVES=16|8|4 forces one (measurement knob).
+// (measured); vip_bilateral_set_waves / VIP_BIL_WAVES=16|8|4 force one.
 #ifndef VIP_BIL_SMALL_MAX_R
 #define VIP_BIL_SMALL_MAX_R 8
 #endif
 inline int small_frame_waves(int tiles_x, int out_rows) {
-    static const int forced = [] {
-        const char* e = getenv("VIP_BIL_WAVES");
-        const int w = e ? atoi(e) : 0;
-        return (w == 16 || w == 8 || w == 4) ? w : 0;
-    }();
+    const int forced = bilateral_forced_waves();
     if (forced) return forced;
     const int cus = device_cus();
     const int cand[3] = {16, 8, 4};

@@ -7,6 +7,7 @@
 // reference, run functions are asynchronous on the caller's stream and return a
 // status instead of printing it.
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -104,6 +105,15 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     std::memcpy(a.ws, wsq, sizeof(a.ws));
 }
 
+// vip_bilateral_set_waves: one process-wide value, read by every bilateral launcher
+static bool valid_waves(int w) { return w == 0 || w == 16 || w == 8 || w == 4; }
+static std::atomic<int> g_bil_waves{[] {
+    const char* e = getenv("VIP_BIL_WAVES");
+    const int w = e ? atoi(e) : 0;
+    return valid_waves(w) ? w : 0;
+}()};
+int bilateral_forced_waves() { return g_bil_waves.load(std::memory_order_relaxed); }
+
 }  // namespace vip
 
 using namespace vip;
@@ -136,6 +146,12 @@ extern "C" {
 
 int vip_abi_version(void) { return VIP_ABI_VERSION; }
 int vip_max_radius(void) { return kMaxRadius; }
+
+int vip_bilateral_set_waves(int waves) {
+    if (!valid_waves(waves)) return VIP_ERR_INVALID_ARGUMENT;
+    g_bil_waves.store(waves, std::memory_order_relaxed);
+    return 0;
+}
 
 const char* vip_error_string(int code) {
     switch (code) {

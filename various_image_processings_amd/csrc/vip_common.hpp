@@ -77,4 +77,7 @@ inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned 
     devs.fetch_or(bit, std::memory_order_relaxed);
     return 0;
 }
+
+// vip_bilateral_set_waves (vip_capi.hip): 0 = per-launch choice, else 16 / 8 / 4.
+int bilateral_forced_waves();
 }  // namespace vip

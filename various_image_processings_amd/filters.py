@@ -29,6 +29,7 @@ from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
 __all__ = [
     "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
     "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
+    "set_bilateral_waves",
 ]
 
 
@@ -73,6 +74,14 @@ def _stream(stream) -> Optional[int]:
 
 def device_synchronize() -> None:
     call("vip_device_synchronize")
+
+
+def set_bilateral_waves(waves: int = 0) -> None:
+    """Process-wide tuning knob (include/vip.h vip_bilateral_set_waves; no reference
+    counterpart): waves per workgroup of the plain bilateral kernel for radius <= 8.
+    0 = chosen per launch (small frames take smaller tiles), or 16 / 8 / 4. Outputs are
+    identical for every setting."""
+    call("vip_bilateral_set_waves", int(waves))
 
 
 class _Handle:
