@@ -205,8 +205,13 @@ constexpr int lut_copies() {
     if (!VIP_JBF_LUT16 || PLANES == 1) return 32;
     return pick_waves<R, PLANES, VIP_JBF_MAXW, 768 * 16, P>() > pick_waves<R, PLANES, 16, 768 * 32, P>() ? 16 : 32;
 }
+// Plain filter above radius 8 (the row-loop radii, C5's r=15): wave cap (build knob;
+// 12 waves allow 168 VGPRs, no spills)
+#ifndef VIP_BIL_BIG_MAXW
+#define VIP_BIL_BIG_MAXW 16
+#endif
 template <int R, int PLANES>
-constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : 16; }
+constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : (R > 8 ? VIP_BIL_BIG_MAXW : 16); }
 
 #ifndef VIP_JBF_SHORT_LUT  // joint kernel: 32-entry clamped LUT when the colour LUT allows it
 #define VIP_JBF_SHORT_LUT 0
