@@ -39,6 +39,20 @@ def test_abi_constants():
     assert L.vip_error_string(0) == b"success"
 
 
+def test_bilateral_wave_knob_validates():
+    """vip_bilateral_set_waves is host state only (no device call): 0 / 16 / 8 / 4 are
+    accepted, anything else is VIP_ERR_INVALID_ARGUMENT."""
+    import various_image_processings_amd as vip
+    L = vip.lib()
+    try:
+        for w in (16, 8, 4, 0):
+            assert L.vip_bilateral_set_waves(w) == 0
+        for w in (12, 2, -1, 32):
+            assert L.vip_bilateral_set_waves(w) == 10001
+    finally:
+        L.vip_bilateral_set_waves(0)
+
+
 def test_reference_api_surface():
     """Same names and defaults as include/cuda/*.hpp of the reference."""
     import various_image_processings_amd as vip
