@@ -32,7 +32,7 @@ extern "C" {
 
 /* argument errors (hipError_t values stay below 1000) */
 #define VIP_ERR_INVALID_ARGUMENT 10001 /* null handle/pointer, non-positive size */
-#define VIP_ERR_UNSUPPORTED_KSIZE 10002 /* ksize even, < 3, or radius above the compiled set */
+#define VIP_ERR_UNSUPPORTED_KSIZE 10002 /* ksize outside what the reference runs: see vip_max_ksize */
 #define VIP_ERR_ALIASING 10003 /* dst aliases src or guide (the kernels read neighbours other blocks write) */
 
 typedef struct vip_bilateral_s* vip_bilateral_t;
@@ -41,8 +41,29 @@ typedef struct vip_texture_s* vip_texture_t;
 
 int vip_abi_version(void);
 const char* vip_error_string(int code);
-/* Largest filter radius (ksize/2) the bilateral / adaptive kernels are compiled for. */
+/* Largest filter radius (ksize/2) any filter accepts (32: bilateral ksize 65). */
 int vip_max_radius(void);
+
+/* Largest ksize each filter accepts: what the reference runs. Its kernels size dynamic
+ * shared memory from ksize with no cap against CUDA's 48 KB default
+ * (src/bilateral_filter_impl.cu:252-254, 272-275; src/adaptive_bilateral_filter_impl.cu:165-167),
+ * so: bilateral 65, joint bilateral 47, adaptive 63, texture 24 (its JBF is 2k-1 <= 47).
+ * Bilateral, joint and adaptive take odd ksize from 1 (radius 0: output = input for
+ * sigma_space > 0); the texture filter any ksize from 1. The C++ and Python layers take
+ * the same sets. Returns VIP_ERR_INVALID_ARGUMENT for an unknown filter. */
+#define VIP_FILTER_BILATERAL 0
+#define VIP_FILTER_JOINT 1
+#define VIP_FILTER_ADAPTIVE 2
+#define VIP_FILTER_TEXTURE 3
+int vip_max_ksize(int filter);
+
+/* Kernel selection, process-wide (no reference counterpart; results are identical either
+ * way). AUTO: radius-specialised kernels for radius 1..15, the runtime-radius kernel for
+ * radius 0 and 16..32. RUNTIME: the runtime-radius kernel for every radius (test and
+ * measurement knob). The environment variable VIP_STENCIL_PATH=1 sets RUNTIME at load. */
+#define VIP_PATH_AUTO 0
+#define VIP_PATH_RUNTIME 1
+int vip_set_stencil_path(int path);
 
 /* ---- device buffers: replaces DeviceImage<T> (include/cuda/device_image.hpp:4-16,
  *      src/device_image.cu:5-52) ---- */
@@ -120,6 +141,10 @@ int vip_gradient_f32(const float* d_src, float* d_dst, int width, int height, in
  *      (include/cuda/bilateral_texture_filter.hpp:7-17, src/bilateral_texture_filter_impl.cu:179-275) ---- */
 int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int nitr, int numerics);
 int vip_texture_destroy(vip_texture_t h);
+/* Device bytes a texture handle of this frame size allocates for its frames: two
+ * ping-pong frames and the guide, u8x3 each (the reference's Impl also held f32
+ * magnitude, blurred and rtv buffers, 20 B/px; no f32 scratch is held here). */
+size_t vip_texture_scratch_bytes(int width, int height);
 /* Impl::execute (:199-214); d_src and d_dst are dense width*3. The handle owns scratch
  * frames (like the reference's Impl): runs on one handle must not overlap, so frames in
  * flight on several streams take one handle per stream. Bilateral and adaptive handles

@@ -12,7 +12,7 @@ from conftest import ROOT
 
 def _header_symbols():
     text = open(os.path.join(ROOT, "include", "vip.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(vip_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(vip_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -34,9 +34,52 @@ def test_abi_constants():
     import various_image_processings_amd as vip
     L = vip.lib()
     assert L.vip_abi_version() == 1
-    assert L.vip_max_radius() == 15
+    assert L.vip_max_radius() == 32
     assert b"ksize" in L.vip_error_string(10002)
     assert L.vip_error_string(0) == b"success"
+
+
+def test_max_ksize_is_what_the_reference_runs():
+    """The reference sizes dynamic shared memory from ksize with no cap, against CUDA's
+    48 KB default (src/bilateral_filter_impl.cu:252-254, 272-275;
+    src/adaptive_bilateral_filter_impl.cu:165-167): the largest ksize whose launch fits
+    is what it runs. Recompute that bound from the reference's own smem formulas."""
+    import various_image_processings_amd as vip
+    L = vip.lib()
+    smem = {  # bytes at ksize k: LUTs (k^2 + table) floats + (32 + k - 1)^2 * 3 per tile plane
+        vip.VIP_FILTER_BILATERAL: lambda k: (k * k + 768) * 4 + (31 + k) ** 2 * 3,
+        vip.VIP_FILTER_JOINT: lambda k: (k * k + 768) * 4 + 2 * (31 + k) ** 2 * 3,
+        vip.VIP_FILTER_ADAPTIVE: lambda k: (k * k + 1536) * 4 + (31 + k) ** 2 * 3,
+    }
+    for f, fn in smem.items():
+        kmax = max(k for k in range(1, 200, 2) if fn(k) <= 48 * 1024)
+        assert L.vip_max_ksize(f) == kmax, (f, kmax)
+    # texture: its JBF runs ksize 2k - 1 (src/bilateral_texture_filter_impl.cu:188)
+    assert L.vip_max_ksize(vip.VIP_FILTER_TEXTURE) == (L.vip_max_ksize(vip.VIP_FILTER_JOINT) + 1) // 2 == 24
+    assert L.vip_max_ksize(7) == 10001
+    # ksize/2 of the largest accepted ksize
+    assert L.vip_max_radius() == L.vip_max_ksize(vip.VIP_FILTER_BILATERAL) // 2
+
+
+def test_stencil_path_knob_validates():
+    import various_image_processings_amd as vip
+    L = vip.lib()
+    try:
+        assert L.vip_set_stencil_path(vip.VIP_PATH_RUNTIME) == 0
+        assert L.vip_set_stencil_path(vip.VIP_PATH_AUTO) == 0
+        assert L.vip_set_stencil_path(2) == 10001
+    finally:
+        L.vip_set_stencil_path(vip.VIP_PATH_AUTO)
+
+
+def test_texture_handle_holds_three_u8_frames():
+    """A texture handle allocates two ping-pong frames and the guide (u8x3), no f32
+    scratch: 75 MB at 4K instead of the reference Impl's 241 MB
+    (src/bilateral_texture_filter_impl.cu:189-194)."""
+    import various_image_processings_amd as vip
+    L = vip.lib()
+    assert L.vip_texture_scratch_bytes(3840, 2160) == 3 * 3840 * 2160 * 3
+    assert L.vip_texture_scratch_bytes(0, 10) == 0
 
 
 def test_bilateral_wave_knob_validates():

@@ -280,7 +280,7 @@ def test_argument_errors(dev):
         vip.CudaBilateralFilter(10, 10, 8)
     assert e.value.code == 10002
     with pytest.raises(vip.VipError):
-        vip.CudaBilateralFilter(10, 10, 33)
+        vip.CudaBilateralFilter(10, 10, 67)
     f = vip.CudaBilateralFilter(10, 10, 3)
     d = dev.empty((10, 10, 3))
     with pytest.raises(vip.VipError) as e:
@@ -512,6 +512,24 @@ def test_device_buffer_validation(dev):
     impl = _BilateralImpl(64, 32, 9)
     with pytest.raises(vip.VipError):  # C ABI: row range outside the handle's rows
         impl.run_rows(dev.empty((40, 64, 3)), good, 8, 0, 0, 40)
+    # DeviceImage carries its dtype: a float32 image is not a u8 frame
+    f32img = vip.DeviceImage(64, 32, 3, "float32")
+    with pytest.raises(ValueError):
+        f.bilateral_filter(f32img, good)
+
+
+def test_gradient_takes_dtype_from_device_image(dev, oracle):
+    """cuda_gradient picks the f32 kernel for a float32 DeviceImage (the reference's
+    template argument T), not the u8 one."""
+    src = oracle.random_f32(40 * 30 * 3).reshape(30, 40, 3)
+    d_src = vip.DeviceImage(40, 30, 3, "float32")
+    d_src.upload(src)
+    d_dst = vip.DeviceImage(40, 30, 1, "float32")
+    vip.cuda_gradient(d_src, d_dst, 40, 30, 3)
+    vip.device_synchronize()
+    got = np.empty((30, 40), np.float32)
+    d_dst.download(got)
+    assert np.array_equal(got, oracle.gradient(src))
 
 
 @pytest.mark.parametrize("kind", ["bilateral", "adaptive", "texture"])

@@ -5,7 +5,17 @@ yuyuyu-bot/various_image_processings, behind that project's include/cuda API.
 The compute runs only in libvip_hip.so (hand-written HIP kernels); this package
 is the host-side mirror of the reference interface. See DESIGN.md.
 """
-from ._lib import LIB_PATH, VipError, lib  # noqa: F401
+from ._lib import (  # noqa: F401
+    LIB_PATH,
+    VIP_FILTER_ADAPTIVE,
+    VIP_FILTER_BILATERAL,
+    VIP_FILTER_JOINT,
+    VIP_FILTER_TEXTURE,
+    VIP_PATH_AUTO,
+    VIP_PATH_RUNTIME,
+    VipError,
+    lib,
+)
 from .filters import (  # noqa: F401
     VIP_NUMERICS_CPP,
     VIP_NUMERICS_CUDA,
@@ -15,7 +25,9 @@ from .filters import (  # noqa: F401
     DeviceImage,
     cuda_gradient,
     device_synchronize,
+    max_ksize,
     set_bilateral_waves,
+    set_stencil_path,
 )
 
 __version__ = "0.1.0"

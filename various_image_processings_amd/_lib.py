@@ -19,6 +19,8 @@ VIP_NUMERICS_CPP = 1
 VIP_ERR_INVALID_ARGUMENT = 10001
 VIP_ERR_UNSUPPORTED_KSIZE = 10002
 VIP_ERR_ALIASING = 10003
+VIP_FILTER_BILATERAL, VIP_FILTER_JOINT, VIP_FILTER_ADAPTIVE, VIP_FILTER_TEXTURE = 0, 1, 2, 3
+VIP_PATH_AUTO, VIP_PATH_RUNTIME = 0, 1
 
 _c_void_p = ctypes.c_void_p
 _c_int = ctypes.c_int
@@ -30,6 +32,9 @@ SIGNATURES = {
     "vip_abi_version": (_c_int, []),
     "vip_error_string": (ctypes.c_char_p, [_c_int]),
     "vip_max_radius": (_c_int, []),
+    "vip_max_ksize": (_c_int, [_c_int]),
+    "vip_set_stencil_path": (_c_int, [_c_int]),
+    "vip_texture_scratch_bytes": (_c_size_t, [_c_int, _c_int]),
     "vip_malloc": (_c_int, [ctypes.POINTER(_c_void_p), _c_size_t]),
     "vip_free": (_c_int, [_c_void_p]),
     "vip_upload": (_c_int, [_c_void_p, _c_void_p, _c_size_t]),

@@ -45,18 +45,51 @@ int launch_texture_iteration_fused(const StencilArgs& a, int ksize, bool cpp, hi
 // coefficient, std::exp(float) == expf). CPP profile: include/cpp/bilateral_filter.hpp:13-36
 // (double coefficient, exp, stored as float). `2 * sigma * sigma` is a float
 // expression in both.
-static void build_space_q(int radius, float sigma_space, int numerics, float* wsq /* kWsStride^2 */) {
+static float space_weight(int r2, float sigma_space, int numerics) {
     const float two_s2 = 2 * sigma_space * sigma_space;
     const float cf = -1.f / two_s2;
     const double cd = -1. / (double)two_s2;
+    return numerics == VIP_NUMERICS_CPP ? (float)std::exp((double)r2 * cd) : expf((float)r2 * cf);
+}
+
+// Quadrant table ws[|ky|][|kx|] of the templated kernels (radius <= kMaxRadius)
+static void build_space_q(int radius, float sigma_space, int numerics, float* wsq /* kWsStride^2 */) {
     for (int i = 0; i < kWsStride * kWsStride; ++i) wsq[i] = 0.f;
+    if (radius > kMaxRadius) return;  // the runtime-radius kernel reads its own table
     for (int ky = 0; ky <= radius; ++ky)
         for (int kx = 0; kx <= radius; ++kx) {
             const int r2 = kx * kx + ky * ky;
             if (r2 > radius * radius) continue;
-            wsq[ky * kWsStride + kx] =
-                numerics == VIP_NUMERICS_CPP ? (float)std::exp((double)r2 * cd) : expf((float)r2 * cf);
+            wsq[ky * kWsStride + kx] = space_weight(r2, sigma_space, numerics);
         }
+}
+
+// Tables of the runtime-radius kernel (vip_stencil_rt.hip), one device allocation:
+// (2R+1) rows of wst floats, row ky + R holding ws(kx, ky) at kx + ra for kx in
+// [-ra, ra + 8) (zero outside the disc), then the R+1 disc half-widths as ints.
+struct RtTables {
+    float* d = nullptr;
+    int wst = 0, ra = 0;
+};
+static int upload_rt_tables(int radius, float sigma_space, int numerics, RtTables* t) {
+    t->ra = round_up(radius, 4);
+    t->wst = 2 * t->ra + 8;
+    const int rows = 2 * radius + 1;
+    const size_t nf = (size_t)rows * t->wst;
+    float* host = (float*)calloc(nf + radius + 1, sizeof(float));
+    if (!host) return (int)hipErrorOutOfMemory;
+    int* hw = reinterpret_cast<int*>(host + nf);
+    for (int ky = -radius; ky <= radius; ++ky) {
+        const int h = isqrt_floor(radius * radius - ky * ky);
+        if (ky >= 0) hw[ky] = h;
+        for (int kx = -h; kx <= h; ++kx)
+            host[(size_t)(ky + radius) * t->wst + kx + t->ra] = space_weight(kx * kx + ky * ky, sigma_space, numerics);
+    }
+    const size_t bytes = (nf + radius + 1) * sizeof(float);
+    int rc = (int)hipMalloc(reinterpret_cast<void**>(&t->d), bytes);
+    if (!rc) rc = (int)hipMemcpy(t->d, host, bytes, hipMemcpyHostToDevice);
+    free(host);
+    return rc;
 }
 
 static void build_color(int len, float sigma_color, int numerics, float* out) {
@@ -67,7 +100,25 @@ static void build_color(int len, float sigma_color, int numerics, float* out) {
         out[i] = numerics == VIP_NUMERICS_CPP ? (float)std::exp((double)(i * i) * cd) : expf((float)(i * i) * cf);
 }
 
-static bool valid_ksize(int ksize) { return ksize >= 3 && (ksize & 1) && ksize / 2 <= kMaxRadius; }
+// The largest ksize the reference runs for each filter: its kernels size dynamic
+// shared memory from ksize with no cap, against CUDA's 48 KB default
+// (src/bilateral_filter_impl.cu:252-254 and :272-275, src/adaptive_bilateral_filter_impl.cu:165-167;
+// the texture filter's JBF is ksize 2k-1, src/bilateral_texture_filter_impl.cu:188).
+// Even ksizes stay rejected: the reference sizes its tile for ksize - 1 halo columns but
+// reads 2 * (ksize / 2), past the tile.
+constexpr int kMaxKsizeBilateral = 65, kMaxKsizeJoint = 47, kMaxKsizeAdaptive = 63, kMaxKsizeTexture = 24;
+static bool valid_ksize(int ksize, int max_ksize) { return ksize >= 1 && (ksize & 1) && ksize <= max_ksize; }
+
+// vip_set_stencil_path: VIP_PATH_AUTO (templated kernels for radius 1..15, the
+// runtime-radius kernel for 0 and 16..32) or VIP_PATH_RUNTIME (the runtime-radius
+// kernel for every radius; a test and measurement knob). Process-wide.
+static std::atomic<int> g_stencil_path{[] {
+    const char* e = getenv("VIP_STENCIL_PATH");
+    return e && atoi(e) == VIP_PATH_RUNTIME ? VIP_PATH_RUNTIME : VIP_PATH_AUTO;
+}()};
+static bool use_runtime_kernel(int radius) {
+    return radius == 0 || radius > kMaxRadius || g_stencil_path.load(std::memory_order_relaxed) == VIP_PATH_RUNTIME;
+}
 
 // Returns the number of leading entries up to the last nonzero one in *nonzero.
 static int upload_color(float** d_color, int len, float sigma_color, int numerics, int* nonzero) {
@@ -122,30 +173,77 @@ struct vip_bilateral_s {
     int width, height, ksize, radius, numerics, lut_nonzero;
     float* d_color;
     float* d_fold;  // joint kernel's folded tables (small sigma_color, radius <= kFoldMaxR), or null
+    RtTables rt;    // runtime-radius kernel tables
     float wsq[kWsStride * kWsStride];
 };
 
 struct vip_adaptive_s {
     int width, height, ksize, radius, numerics, lut_nonzero;
     float* d_color;
+    RtTables rt;
     float wsq[kWsStride * kWsStride];
 };
 
+// The handle owns three u8x3 frames: the two ping-pong frames and the guide. The
+// reference's Impl also holds f32 magnitude, blurred and rtv buffers
+// (src/bilateral_texture_filter_impl.cu:189-194, 20 B/px); here the guide stage keeps
+// them in LDS, and the stage entry points (vip_texture_blur_rtv / _guide) write the
+// caller's buffers, so the handle holds none.
 struct vip_texture_s {
     int width, height, ksize, nitr, numerics;
     int mode;  // VIP_TEXTURE_TWO_LAUNCH or VIP_TEXTURE_FUSED (vip_texture_set_mode)
     vip_bilateral_t jbf;
     uint8_t* d_ping[2];
     uint8_t* d_guide;
-    float* d_mag;
-    float* d_blurred;
-    float* d_rtv;
 };
+
+static RtArgs rt_args(const RtTables& t, int radius, int width, const uint8_t* src, size_t src_pitch,
+                      const uint8_t* guide, size_t guide_pitch, uint8_t* dst, size_t dst_pitch, int out_rows,
+                      int src_row0, int row_lo, int row_hi, const float* d_color) {
+    RtArgs a{};
+    a.src = src;
+    a.guide = guide;
+    a.dst = dst;
+    a.src_pitch = (long long)src_pitch;
+    a.guide_pitch = (long long)guide_pitch;
+    a.dst_pitch = (long long)dst_pitch;
+    a.width = width;
+    a.out_rows = out_rows;
+    a.src_row0 = src_row0;
+    a.row_lo = row_lo;
+    a.row_hi = row_hi;
+    const auto al4 = [](const void* p, size_t pitch) { return ((uintptr_t)p % 4 == 0) && (pitch % 4 == 0); };
+    a.aligned = al4(src, src_pitch) && al4(guide, guide_pitch);
+    a.dst_aligned = ((uintptr_t)dst % 4 == 0) && (dst_pitch % 4 == 0);
+    a.color = d_color;
+    a.wsrow = t.d;
+    a.hw = reinterpret_cast<const int*>(t.d + (size_t)(2 * radius + 1) * t.wst);
+    a.R = radius;
+    a.wst = t.wst;
+    a.ra = t.ra;
+    return a;
+}
 
 extern "C" {
 
 int vip_abi_version(void) { return VIP_ABI_VERSION; }
-int vip_max_radius(void) { return kMaxRadius; }
+int vip_max_radius(void) { return kRtMaxRadius; }
+
+int vip_max_ksize(int filter) {
+    switch (filter) {
+        case VIP_FILTER_BILATERAL: return kMaxKsizeBilateral;
+        case VIP_FILTER_JOINT: return kMaxKsizeJoint;
+        case VIP_FILTER_ADAPTIVE: return kMaxKsizeAdaptive;
+        case VIP_FILTER_TEXTURE: return kMaxKsizeTexture;
+        default: return VIP_ERR_INVALID_ARGUMENT;
+    }
+}
+
+int vip_set_stencil_path(int path) {
+    if (path != VIP_PATH_AUTO && path != VIP_PATH_RUNTIME) return VIP_ERR_INVALID_ARGUMENT;
+    g_stencil_path.store(path, std::memory_order_relaxed);
+    return 0;
+}
 
 int vip_bilateral_set_waves(int waves) {
     if (!valid_waves(waves)) return VIP_ERR_INVALID_ARGUMENT;
@@ -157,7 +255,8 @@ const char* vip_error_string(int code) {
     switch (code) {
         case 0: return "success";
         case VIP_ERR_INVALID_ARGUMENT: return "invalid argument";
-        case VIP_ERR_UNSUPPORTED_KSIZE: return "unsupported ksize (must be odd, 3..31)";
+        case VIP_ERR_UNSUPPORTED_KSIZE:
+            return "unsupported ksize (odd, 1..65 bilateral, 1..47 joint bilateral, 1..63 adaptive; texture 1..24)";
         case VIP_ERR_ALIASING: return "source and destination alias";
         default: return hipGetErrorString((hipError_t)code);
     }
@@ -230,7 +329,7 @@ static int upload_fold(vip_bilateral_s* h, float sigma_color) {
 int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
                          int numerics) {
     if (!out || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
-    if (!valid_ksize(ksize)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    if (!valid_ksize(ksize, kMaxKsizeBilateral)) return VIP_ERR_UNSUPPORTED_KSIZE;
     auto* h = new (std::nothrow) vip_bilateral_s();
     if (!h) return (int)hipErrorOutOfMemory;
     h->width = width;
@@ -240,6 +339,7 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
     h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
     int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics, &h->lut_nonzero);
+    if (!rc) rc = upload_rt_tables(h->radius, sigma_space, h->numerics, &h->rt);
     if (!rc && h->lut_nonzero <= 31 && h->radius <= kFoldMaxR) rc = upload_fold(h, sigma_color);
     if (rc) {
         vip_bilateral_destroy(h);
@@ -252,6 +352,7 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
 int vip_bilateral_destroy(vip_bilateral_t h) {
     if (!h) return 0;
     if (h->d_fold) (void)hipFree(h->d_fold);
+    if (h->rt.d) (void)hipFree(h->rt.d);
     const int rc = h->d_color ? (int)hipFree(h->d_color) : 0;
     delete h;
     return rc;
@@ -266,6 +367,13 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
         return VIP_ERR_INVALID_ARGUMENT;
     if (d_dst == d_src || (d_guide && d_dst == d_guide)) return VIP_ERR_ALIASING;
     const bool joint = d_guide != nullptr;
+    if (joint && h->ksize > kMaxKsizeJoint) return VIP_ERR_UNSUPPORTED_KSIZE;
+    if (use_runtime_kernel(h->radius)) {
+        const RtArgs r = rt_args(h->rt, h->radius, h->width, d_src, src_pitch, joint ? d_guide : d_src,
+                                 joint ? guide_pitch : src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo,
+                                 row_hi, h->d_color);
+        return launch_stencil_rt(r, joint, false, h->numerics == VIP_NUMERICS_CUDA, (hipStream_t)stream);
+    }
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, joint ? d_guide : d_src, joint ? guide_pitch : src_pitch, d_dst,
               dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, joint ? h->d_fold : nullptr,
@@ -291,7 +399,7 @@ int vip_joint_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_
 int vip_adaptive_create(vip_adaptive_t* out, int width, int height, int ksize, float sigma_space, float sigma_color,
                         int numerics) {
     if (!out || width <= 0 || height <= 0) return VIP_ERR_INVALID_ARGUMENT;
-    if (!valid_ksize(ksize)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    if (!valid_ksize(ksize, kMaxKsizeAdaptive)) return VIP_ERR_UNSUPPORTED_KSIZE;
     auto* h = new (std::nothrow) vip_adaptive_s();
     if (!h) return (int)hipErrorOutOfMemory;
     h->width = width;
@@ -301,9 +409,10 @@ int vip_adaptive_create(vip_adaptive_t* out, int width, int height, int ksize, f
     h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
     // the reference's table is 512*3 long (src/adaptive_bilateral_filter_impl.cu:5)
-    const int rc = upload_color(&h->d_color, 1536, sigma_color, h->numerics, &h->lut_nonzero);
+    int rc = upload_color(&h->d_color, 1536, sigma_color, h->numerics, &h->lut_nonzero);
+    if (!rc) rc = upload_rt_tables(h->radius, sigma_space, h->numerics, &h->rt);
     if (rc) {
-        delete h;
+        vip_adaptive_destroy(h);
         return rc;
     }
     *out = h;
@@ -312,7 +421,8 @@ int vip_adaptive_create(vip_adaptive_t* out, int width, int height, int ksize, f
 
 int vip_adaptive_destroy(vip_adaptive_t h) {
     if (!h) return 0;
-    const int rc = (int)hipFree(h->d_color);
+    if (h->rt.d) (void)hipFree(h->rt.d);
+    const int rc = h->d_color ? (int)hipFree(h->d_color) : 0;
     delete h;
     return rc;
 }
@@ -322,6 +432,11 @@ int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pit
     if (!h || !d_src || !d_dst || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi)
         return VIP_ERR_INVALID_ARGUMENT;
     if (d_dst == d_src) return VIP_ERR_ALIASING;
+    if (use_runtime_kernel(h->radius)) {
+        const RtArgs r = rt_args(h->rt, h->radius, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch,
+                                 out_rows, src_row0, row_lo, row_hi, h->d_color);
+        return launch_stencil_rt(r, false, true, h->numerics == VIP_NUMERICS_CUDA, (hipStream_t)stream);
+    }
     StencilArgs a;
     fill_args(a, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo, row_hi,
               h->d_color, h->lut_nonzero, nullptr, h->wsq);
@@ -356,17 +471,15 @@ int vip_texture_destroy(vip_texture_t h) {
     (void)hipFree(h->d_ping[0]);
     (void)hipFree(h->d_ping[1]);
     (void)hipFree(h->d_guide);
-    (void)hipFree(h->d_mag);
-    (void)hipFree(h->d_blurred);
-    (void)hipFree(h->d_rtv);
     delete h;
     return 0;
 }
 
 int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int nitr, int numerics) {
-    if (!out || width <= 0 || height <= 0 || nitr < 0 || ksize < 1) return VIP_ERR_INVALID_ARGUMENT;
-    // the embedded JBF has ksize 2k-1 (src/bilateral_texture_filter_impl.cu:188)
-    if (!valid_ksize(2 * ksize - 1)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    if (!out || width <= 0 || height <= 0 || nitr < 0) return VIP_ERR_INVALID_ARGUMENT;
+    // any ksize 1..24 (even too); the embedded JBF has ksize 2k-1 <= 47
+    // (src/bilateral_texture_filter_impl.cu:188)
+    if (ksize < 1 || ksize > kMaxKsizeTexture) return VIP_ERR_UNSUPPORTED_KSIZE;
     auto* h = new (std::nothrow) vip_texture_s();
     if (!h) return (int)hipErrorOutOfMemory;
     h->width = width;
@@ -374,21 +487,23 @@ int vip_texture_create(vip_texture_t* out, int width, int height, int ksize, int
     h->ksize = ksize;
     h->nitr = nitr;
     h->numerics = numerics == VIP_NUMERICS_CPP ? VIP_NUMERICS_CPP : VIP_NUMERICS_CUDA;
-    const size_t n = (size_t)width * height;
+    const size_t frame = vip_texture_scratch_bytes(width, height) / 3;
     int rc = vip_bilateral_create(&h->jbf, width, height, 2 * ksize - 1, (float)(ksize - 1), 1.73205080757f,
                                   h->numerics);
-    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_ping[0]), n * 3);
-    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_ping[1]), n * 3);
-    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_guide), n * 3);
-    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_mag), n * sizeof(float));
-    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_blurred), n * 3 * sizeof(float));
-    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_rtv), n * sizeof(float));
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_ping[0]), frame);
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_ping[1]), frame);
+    if (!rc) rc = (int)hipMalloc(reinterpret_cast<void**>(&h->d_guide), frame);
     if (rc) {
         vip_texture_destroy(h);
         return rc;
     }
     *out = h;
     return 0;
+}
+
+size_t vip_texture_scratch_bytes(int width, int height) {
+    if (width <= 0 || height <= 0) return 0;
+    return 3 * ((size_t)width * height * 3);  // two ping-pong frames + the guide, u8x3 each
 }
 
 int vip_texture_set_mode(vip_texture_t h, int mode) {

@@ -48,6 +48,26 @@ struct StencilArgs {
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 
+// Runtime-radius kernel (vip_stencil_rt.hip): radius 0 and the radii above the
+// templated set, up to the reference's largest (bilateral ksize 65).
+constexpr int kRtMaxRadius = 32;
+
+struct RtArgs {
+    const uint8_t* src;
+    const uint8_t* guide;  // == src for the plain filters
+    uint8_t* dst;
+    long long src_pitch, guide_pitch, dst_pitch;
+    int width, out_rows, src_row0, row_lo, row_hi;  // as StencilArgs
+    int aligned, dst_aligned;
+    const float* color;    // colour LUT (768 or 1536 entries)
+    const float* wsrow;    // [2R+1][wst]: ws(kx, ky) at [ky + R][kx + ra], 0 outside the disc
+    const int* hw;         // [R+1]: disc half-width of row |ky|
+    int R, wst, ra;
+    int L, S, tiles_x;     // set by the launcher
+};
+int launch_stencil_rt(const RtArgs& a, bool joint, bool adaptive, bool fma, hipStream_t stream);
+int stencil_rt_max_radius(bool joint, bool adaptive);
+
 // One workgroup per CU of the current device (the 96 KiB LUT fills most of the CU's
 // LDS), each striding over tiles; fewer blocks than CUs when the frame has fewer tiles.
 inline int device_cus() {
@@ -531,9 +551,10 @@ __device__ __forceinline__ void finish_outputs(const f2 (&a01)[P], const f2 (&a2
     }
 }
 
-// Write P RGB outputs (3P bytes) of row oy starting at column x.
-template <int P>
-__device__ __forceinline__ void store_px(const StencilArgs& a, int oy, int x, const uint32_t (&o)[P]) {
+// Write P RGB outputs (3P bytes) of row oy starting at column x (A: StencilArgs or
+// RtArgs -- out_rows, width, dst, dst_pitch, dst_aligned).
+template <int P, class A>
+__device__ __forceinline__ void store_px(const A& a, int oy, int x, const uint32_t (&o)[P]) {
     if (oy >= a.out_rows || x >= a.width) return;
     uint8_t* row = a.dst + (long long)oy * a.dst_pitch;
     if constexpr (P == 4) {

@@ -829,7 +829,7 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int 
 template <bool CPP>
 static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
                        int aligned, hipStream_t s) {
-    switch (ksize / 2) {
+    switch (ksize / 2) {  // ksize 1..24 (kMaxKsizeTexture)
         case 1: return launch_gf<1, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         case 2: return launch_gf<2, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         case 3: return launch_gf<3, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
@@ -837,7 +837,12 @@ static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width,
         case 5: return launch_gf<5, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         case 6: return launch_gf<6, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         case 7: return launch_gf<7, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 0: return launch_gf<0, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         case 8: return launch_gf<8, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 9: return launch_gf<9, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 10: return launch_gf<10, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 11: return launch_gf<11, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+        case 12: return launch_gf<12, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         default: return VIP_ERR_UNSUPPORTED_KSIZE;
     }
 }

@@ -29,7 +29,7 @@ from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
 __all__ = [
     "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
     "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
-    "set_bilateral_waves",
+    "set_bilateral_waves", "set_stencil_path", "max_ksize",
 ]
 
 
@@ -43,6 +43,8 @@ def _ptr(buf, nbytes: int = 0, dtype: str = "uint8") -> int:
     if isinstance(buf, int):
         return buf
     if isinstance(buf, DeviceImage):
+        if buf.dtype != dtype:
+            raise ValueError(f"expected a {dtype} DeviceImage, got {buf.dtype}")
         if buf.nbytes < nbytes:
             raise ValueError(f"DeviceImage of {buf.nbytes} bytes, {nbytes} needed")
         return buf.get()
@@ -74,6 +76,20 @@ def _stream(stream) -> Optional[int]:
 
 def device_synchronize() -> None:
     call("vip_device_synchronize")
+
+
+def set_stencil_path(path: int = _lib.VIP_PATH_AUTO) -> None:
+    """Process-wide kernel selection (include/vip.h vip_set_stencil_path; no reference
+    counterpart): VIP_PATH_AUTO (radius-specialised kernels for radius 1..15, the
+    runtime-radius kernel for 0 and 16..32) or VIP_PATH_RUNTIME (the runtime-radius
+    kernel for every radius). Outputs are identical either way."""
+    call("vip_set_stencil_path", int(path))
+
+
+def max_ksize(filter_kind: int) -> int:
+    """Largest ksize a filter accepts (include/vip.h vip_max_ksize): what the reference
+    runs -- bilateral 65, joint 47, adaptive 63, texture 24."""
+    return int(lib().vip_max_ksize(int(filter_kind)))
 
 
 def set_bilateral_waves(waves: int = 0) -> None:
@@ -240,10 +256,13 @@ class CudaBilateralTextureFilter:
 
 
 def cuda_gradient(d_src, d_dst, width, height, src_ch=1, numerics=VIP_NUMERICS_CUDA, stream=None):
-    """include/cuda/gradient.hpp:13-23. dtype (uint8 / float32) is taken from a torch
-    tensor; pass ``src_dtype`` via a tensor, raw addresses are treated as uint8.
-    Asynchronous, like src/gradient_impl.cu:90-103."""
-    is_f32 = hasattr(d_src, "dtype") and str(d_src.dtype) == "torch.float32"
+    """include/cuda/gradient.hpp:13-23. The source dtype (uint8 / float32, the
+    reference's template argument T) is taken from a torch tensor or a DeviceImage; raw
+    addresses are treated as uint8. Asynchronous, like src/gradient_impl.cu:90-103."""
+    if isinstance(d_src, DeviceImage):
+        is_f32 = d_src.dtype == "float32"
+    else:
+        is_f32 = hasattr(d_src, "dtype") and str(d_src.dtype) == "torch.float32"
     name = "vip_gradient_f32" if is_f32 else "vip_gradient_u8"
     n = int(width) * int(height)
     call(name, _ptr(d_src, n * int(src_ch) * (4 if is_f32 else 1), "float32" if is_f32 else "uint8"),
@@ -257,7 +276,8 @@ class DeviceImage:
     _ITEM = {"uint8": 1, "float32": 4}
 
     def __init__(self, width, height, channels=1, dtype="uint8"):
-        self.nbytes = int(width) * int(height) * int(channels) * self._ITEM[str(dtype)]
+        self.dtype = str(dtype)  # the reference's template argument T
+        self.nbytes = int(width) * int(height) * int(channels) * self._ITEM[self.dtype]
         self._p = ctypes.c_void_p()
         call("vip_malloc", ctypes.byref(self._p), self.nbytes)
 
