@@ -1,0 +1,110 @@
+/*
+ * vip_shard.h -- row-sharded frames over several GPUs with an RCCL halo exchange
+ * (C ABI, libvip_shard.so; links libvip_hip.so and RCCL).
+ *
+ * No reference counterpart: yuyuyu-bot/various_image_processings has no multi-device
+ * code. This is the north_star's row-tiled configuration (BASELINE
+ * config 5: bilateral r=15 on 16384x16384 over 8 GPUs, "2r-row halo exchanged via RCCL
+ * sendrecv over xGMI") as a native entry point for C/C++ callers, who would otherwise have
+ * to write their own exchange around vip_bilateral_run_rows. The Python layer
+ * (various_image_processings_amd/sharded.py) drives the same functions.
+ *
+ * Geometry (identical on every rank, sharded.py SlabGeometry): rank i owns frame rows
+ * [row_begin, row_begin + own) of a frame_height-row frame (balanced contiguous split, the
+ * first frame_height % nranks ranks one row more). Its slab is a dense (own + 2r) x width
+ * RGB8 buffer (pitch width * 3): rows [0, r) halo above, [r, r + own) own rows,
+ * [r + own, 2r + own) halo below, r = ksize / 2. The caller fills the own rows; a run
+ * receives the halos from the row neighbours, then filters the own rows into `out`
+ * (own rows, any pitch). At the first / last rank the missing halo is replaced by the
+ * reference's replicate border (reads clamp to the own rows), so the sharded result is
+ * bit-identical to one single-GPU launch over the whole frame.
+ *
+ * Overlap: a run enqueues the exchange on the shard's own communication stream and, at
+ * the same time, the interior rows [r, own - r) (which read only own rows) on the
+ * caller's stream; the two r-row edge bands follow once the halos have arrived.
+ *
+ * Transports: RCCL (one communicator per rank; ncclSend/ncclRecv between row neighbours
+ * in one group, no collective) or LOCAL (all slabs in one process on one device, halos by
+ * device-to-device copies: the same geometry, split and stream ordering, testable on a
+ * single GPU).
+ *
+ * Return value: 0, a hipError_t, a VIP_ERR_* code (vip.h) or VIP_ERR_COMM /
+ * VIP_ERR_COMM_TIMEOUT below. Communicator creation never blocks past its timeout: it
+ * runs RCCL's non-blocking initialisation, polls it until the deadline, then aborts the
+ * communicator and returns VIP_ERR_COMM_TIMEOUT.
+ */
+#ifndef VIP_SHARD_H
+#define VIP_SHARD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "vip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VIP_ERR_COMM 10004         /* an RCCL call failed (vip_shard_last_error) */
+#define VIP_ERR_COMM_TIMEOUT 10005 /* communicator set-up not complete before the timeout */
+
+#define VIP_SHARD_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
+
+#define VIP_SHARD_RCCL 0
+#define VIP_SHARD_LOCAL 1
+
+typedef struct vip_shard_s* vip_shard_t;
+
+/* Balanced contiguous row split: rank's first row and row count (no device call). */
+int vip_shard_rows(int frame_height, int nranks, int rank, int* row_begin, int* own_rows);
+
+/* The communicator id rank 0 creates and the caller broadcasts to every rank
+ * (ncclGetUniqueId); `id` holds VIP_SHARD_ID_BYTES bytes. */
+int vip_shard_unique_id(void* id);
+
+/* One process per GPU: this rank's shard on the current device, filter kind
+ * VIP_FILTER_BILATERAL or VIP_FILTER_ADAPTIVE (vip.h) with the reference's parameters.
+ * Every rank calls it with the same id, nranks and filter arguments; it returns once all
+ * ranks have joined, or VIP_ERR_COMM_TIMEOUT after timeout_ms (<= 0: 180 s).
+ * VIP_ERR_INVALID_ARGUMENT if the thinnest shard is thinner than the halo. */
+int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
+                     float sigma_color, int numerics, int nranks, int rank, const void* id, int timeout_ms);
+
+/* One process, n shards: transport VIP_SHARD_RCCL puts shard i on devices[i] (one RCCL
+ * communicator per device, initialised together -- ncclCommInitAll's pattern);
+ * VIP_SHARD_LOCAL puts all n on the current device (devices ignored). out[n]. */
+int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* devices, int kind, int width,
+                           int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
+                           int timeout_ms);
+
+/* Geometry of a shard: its first frame row, own rows and halo rows (r). */
+int vip_shard_geometry(vip_shard_t h, int* row_begin, int* own_rows, int* halo_rows);
+
+/* One filter application on this rank's slab (multi-process, RCCL). Asynchronous on
+ * `stream`: the slab's own rows must be written before on `stream`; `out` is complete
+ * when `stream` is. Every rank must call it once per frame, in the same order. */
+int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream);
+
+/* As vip_shard_run, with timing events (hipEvent_t, timing enabled, as void*):
+ * events[0] before the run on `stream`, events[1] after the exchange on the shard's
+ * communication stream, events[2] after the interior rows on `stream`, events[3] after
+ * the edge bands on `stream`. */
+int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream,
+                        void* const* events);
+
+/* One filter application of every shard of a group created by vip_shard_create_group
+ * (one process): slabs[i], outs[i] (pitch out_pitch) and streams[i] on shard i's device. */
+int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* const* outs, size_t out_pitch,
+                        void* const* streams);
+
+/* Text of the last RCCL failure on this thread ("" if none). */
+const char* vip_shard_last_error(void);
+
+/* Releases the shard (and its communicator). Group members are destroyed one by one. */
+int vip_shard_destroy(vip_shard_t h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VIP_SHARD_H */

@@ -1,9 +1,11 @@
 // Exactness check of the bilateral epilogue's division (vip_stencil.hpp div_by_sumk):
 //   y  = rcp(k) refined by one Newton step          -- must equal RN(1/k)
 //   q0 = RN(s * y); r = fma(-k, q0, s); q = fma(r, y, q0)  -- must equal RN(s / k)
-// (a) the reciprocal EXHAUSTIVELY for every float k in [1, 2^17) -- the sum of
+// (a) the reciprocal EXHAUSTIVELY for every float k in [1, 2^38) -- the sum of
 //     weights of a bilateral/joint window (the centre tap weighs exactly 1, every
-//     tap at most 1, at most 31*31 taps) and the texture guide's 1 + exp(x) >= 2;
+//     tap at most 1, at most 31*31 taps) and the texture guide's 1 + exp(x) in
+//     [2, 1 + e^25.5] (x = sigma_alpha (rtv - rtv_min) <= 255 / (5 ksize): up to 2^37 at
+//     ksize 2);
 // (b) the quotient for 2^30 pseudo-random (s, k), s in [0, 255 k], and for s at the
 //     float midpoints' neighbourhoods -- Markstein's theorem makes (b) follow from (a),
 //     this is the empirical cross-check.
@@ -95,9 +97,9 @@ __global__ void quot_random(uint64_t base) {
 int main() {
     unsigned long long zero[5] = {0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero)) != hipSuccess) return 2;
-    // bit patterns of 1.0f and 2^17: the epilogue's sums of weights lie in [1, 1024), the
-    // texture guide's 1 + exp(x) in [2, 2^17)
-    const uint32_t lo = 0x3f800000u, hi = 0x48000000u;
+    // bit patterns of 1.0f and 2^38: the epilogue's sums of weights lie in [1, 1024), the
+    // texture guide's 1 + exp(x) in [2, 2^37) (x <= 25.5 at ksize 2)
+    const uint32_t lo = 0x3f800000u, hi = 0x52800000u;
     const uint32_t n = hi - lo;
     hipLaunchKernelGGL(recip_all, dim3((n + 255) / 256), dim3(256), 0, 0, lo, n);
     const uint64_t per = 1ull << 26;
@@ -111,7 +113,7 @@ int main() {
     hipLaunchKernelGGL(exp_all, dim3((nexp + 255) / 256), dim3(256), 0, 0, nexp);
     unsigned long long bad[5];
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
-    std::printf("reciprocal: %u floats k in [1, 2^17), %llu mismatches\n", n, bad[0]);
+    std::printf("reciprocal: %u floats k in [1, 2^38), %llu mismatches\n", n, bad[0]);
     std::printf("quotient: %llu random (s, k), %llu mismatches\n", (unsigned long long)(16 * per), bad[1]);
     std::printf("integer sqrt: %u integers in [0, 2^20), %llu mismatches\n", nsq, bad[2]);
     std::printf("u8 clamp pack: %u floats |v| < 2048 of each sign, %llu mismatches\n", npk, bad[3]);

@@ -141,3 +141,49 @@ def test_sample_links_against_library(name):
     out = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
     line = [l for l in out.splitlines() if "libvip_hip" in l]
     assert line and "not found" not in line[0]
+
+
+def _shard_header_symbols():
+    text = open(os.path.join(ROOT, "include", "vip_shard.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(vip_\w+)\s*\(", text, re.M)))
+
+
+def test_shard_library_exports_and_binds_every_symbol():
+    """libvip_shard.so (include/vip_shard.h) loads here (RCCL without a GPU) and exports
+    every declared entry point; the Python binding declares the same set."""
+    import ctypes
+    from various_image_processings_amd import _shard_lib
+    syms = _shard_header_symbols()
+    assert len(syms) >= 9
+    handle = ctypes.CDLL(_shard_lib.LIB_PATH)
+    assert not [s for s in syms if not hasattr(handle, s)]
+    assert sorted(_shard_lib.SIGNATURES) == syms
+    _shard_lib.lib()
+
+
+def test_native_rows_match_slab_geometry():
+    from various_image_processings_amd.sharded import native_rows, shard_rows
+    for h in (1, 7, 2160, 16384, 16385):
+        for n in (1, 2, 3, 5, 8):
+            if h < n:
+                continue
+            rows = [native_rows(h, n, r) for r in range(n)]
+            assert rows == [shard_rows(h, n, r) for r in range(n)]
+            assert rows[0][0] == 0 and rows[-1][1] == h
+            assert all(a[1] == b[0] for a, b in zip(rows, rows[1:]))
+
+
+def test_shard_create_validates_before_device_work():
+    """Bad kind / thin shards / bad ranks are rejected before any device or RCCL call
+    (no GPU here), identically on every rank."""
+    import ctypes
+    from various_image_processings_amd import _shard_lib as S
+    L = S.lib()
+    h = ctypes.c_void_p()
+    idb = ctypes.create_string_buffer(128)
+    args = lambda kind, fh, k, n, r: (ctypes.byref(h), kind, 64, fh, k, 10.0, 30.0, 0, n, r, idb, 1000)  # noqa: E731
+    assert L.vip_shard_create(*args(3, 100, 15, 2, 0)) == 10001      # texture is not a shard kind
+    assert L.vip_shard_create(*args(0, 100, 31, 8, 0)) == 10001      # 12-row shards < 15-row halo
+    assert L.vip_shard_create(*args(0, 100, 15, 2, 2)) == 10001      # rank outside the world
+    assert L.vip_shard_create(*args(0, 100, 8, 2, 0)) == 10002       # even ksize
+    assert L.vip_shard_create(ctypes.byref(h), 0, 64, 100, 15, 10.0, 30.0, 0, 2, 0, None, 1000) == 10001

@@ -455,7 +455,8 @@ def test_texture_iterate_rows_band(dev, oracle):
 def test_epilogue_division_exact():
     """The bilateral/joint epilogue divides by sumk via one reciprocal (vip_stencil.hpp
     recip_exact/div_by_sumk). microbench/div_check checks RN(1/k) for EVERY float k in
-    [1, 1024) and 2^30 quotients against the IEEE divide on the GPU, the texture
+    [1, 2^38) (the epilogue's sums of weights and the texture guide's 1 + exp(x) at every
+    ksize) and 2^30 quotients against the IEEE divide on the GPU, the texture
     gradient's sqrt_int_exact against sqrtf for every integer in [0, 2^20), and the guide
     blend's pack_u8_clamped against the clamp for every float |v| < 2048."""
     import os

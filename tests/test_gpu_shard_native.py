@@ -1,0 +1,135 @@
+"""The native row-sharding path (include/vip_shard.h, libvip_shard.so) on the GPU.
+
+Sharded output must equal one single-GPU launch over the whole frame, bit for bit:
+* LOCAL transport: n slabs of one frame on the one device, halos by device copies,
+  with the same split (interior rows while the halos move, then the edge bands) and
+  the same stream ordering as the RCCL transport;
+* RCCL transport with one rank (no neighbours; a one-device communicator), both as a
+  one-process group and through the multi-process entry point with a unique id;
+* a communicator whose peer never joins returns VIP_ERR_COMM_TIMEOUT, no hang.
+A multi-rank RCCL exchange needs several GPUs: it runs in the driver's 8-GPU bench.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import various_image_processings_amd as vip
+from various_image_processings_amd import _shard_lib as S
+from various_image_processings_amd.sharded import NativeShard, ShardGroup, native_unique_id
+
+pytestmark = pytest.mark.gpu
+
+
+def _single(dev, img, k, adaptive):
+    h, w, _ = img.shape
+    d = dev.empty((h, w, 3))
+    if adaptive:
+        vip.CudaAdaptiveBilateralFilter(w, h, k).execute(dev.put(img), d)
+    else:
+        vip.CudaBilateralFilter(w, h, k).bilateral_filter(dev.put(img), d)
+    return dev.get(d)
+
+
+def _run_group(dev, img, k, n, adaptive, transport=S.VIP_SHARD_LOCAL, devices=None):
+    torch = dev.torch_
+    h, w, _ = img.shape
+    g = ShardGroup(n, w, h, k, transport=transport, devices=devices, adaptive=adaptive)
+    slabs, outs, streams = [], [], []
+    for geo in g.geos:
+        b, e = geo.rows
+        slab = dev.empty((geo.slab_rows, w, 3))
+        slab.fill_(77)  # the halos are overwritten by the exchange (or unread at the frame edges)
+        slab[geo.radius:geo.radius + geo.own] = dev.put(img[b:e])
+        slabs.append(slab)
+        outs.append(dev.empty((geo.own, w, 3)))
+        streams.append(torch.cuda.Stream())
+    torch.cuda.synchronize()
+    g.filter(slabs, outs, streams)
+    torch.cuda.synchronize()
+    return np.concatenate([dev.get(o) for o in outs])
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_local_group_equals_single_launch_4k(dev, oracle, n, adaptive):
+    img = oracle.random_image(3840, 2160)
+    want = _single(dev, img, 15, adaptive)
+    got = _run_group(dev, img, 15, n, adaptive)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("shape,k,n", [((530, 700), 31, 8), ((77, 300), 9, 5), ((40, 131), 15, 5), ((64, 129), 65, 2)])
+def test_local_group_ragged_vs_oracle(dev, oracle, shape, k, n):
+    """Uneven shards (sizes differ by one), thin shards (own < 2r: no interior rows),
+    the runtime-radius kernel (k = 65), against the oracle."""
+    h, w = shape
+    img = oracle.random_u8(h * w * 3).reshape(h, w, 3)
+    got = _run_group(dev, img, k, n, False)
+    assert np.array_equal(got, oracle.bilateral(img, k))
+
+
+def test_local_group_c5_frame_8_way(dev, oracle):
+    """C5's ksize 31 over a 16384-wide frame, 8 slabs: every pixel equals one launch."""
+    img = oracle.random_image(16384, 2048)
+    assert np.array_equal(_run_group(dev, img, 31, 8, False), _single(dev, img, 31, False))
+
+
+def test_thin_shards_rejected_before_any_device_work(dev):
+    with pytest.raises(vip.VipError) as e:
+        ShardGroup(8, 64, 100, 31)  # 12-row shards < 15-row halo
+    assert e.value.code == 10001
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_rccl_one_device_group(dev, oracle, adaptive):
+    import torch
+    img = oracle.random_image(1000, 600)
+    got = _run_group(dev, img, 15, 1, adaptive, transport=S.VIP_SHARD_RCCL, devices=[torch.cuda.current_device()])
+    assert np.array_equal(got, _single(dev, img, 15, adaptive))
+
+
+def test_rccl_single_rank_native_shard_timed(dev, oracle):
+    """vip_shard_create with a unique id and nranks = 1 (the multi-process entry point),
+    vip_shard_run and vip_shard_run_timed: equal to one launch; events in order."""
+    torch = dev.torch_
+    img = oracle.random_image(900, 500)
+    s = NativeShard(900, 500, 15, 0, 1, native_unique_id())
+    geo = s.geo
+    slab = dev.empty((geo.slab_rows, 900, 3))
+    slab[geo.radius:geo.radius + geo.own] = dev.put(img)
+    out = dev.empty((500, 900, 3))
+    s.filter(slab, out)
+    want = _single(dev, img, 15, False)
+    assert np.array_equal(dev.get(out), want)
+    out.zero_()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    s.filter_timed(slab, out, ev)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.get(out), want)
+    assert ev[0].elapsed_time(ev[3]) > 0
+
+
+def test_rccl_missing_peer_times_out():
+    """A 2-rank communicator whose second rank never joins: vip_shard_create returns
+    VIP_ERR_COMM_TIMEOUT after its timeout instead of blocking (run in a child process
+    with its own limit, so a hang could not stall the suite)."""
+    code = r'''
+import ctypes, sys, time
+sys.path.insert(0, sys.argv[1])
+from various_image_processings_amd import _shard_lib as S
+from various_image_processings_amd.sharded import native_unique_id
+h = ctypes.c_void_p()
+t0 = time.time()
+rc = S.lib().vip_shard_create(ctypes.byref(h), 0, 64, 64, 3, 10.0, 30.0, 0, 2, 0,
+                              ctypes.create_string_buffer(native_unique_id(), 128), 3000)
+print(rc, round(time.time() - t0, 1), S.lib().vip_shard_last_error().decode())
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code, root], capture_output=True, text=True, timeout=90)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    rc, secs = r.stdout.split()[:2]
+    assert int(rc) == S.VIP_ERR_COMM_TIMEOUT, r.stdout
+    assert 2.5 <= float(secs) < 60, r.stdout

@@ -1,0 +1,419 @@
+// Row-sharded frames with an RCCL halo exchange (include/vip_shard.h), host code.
+//
+// No reference counterpart (the reference is single-GPU): the
+// north_star's row-tiled configuration as a native C entry point. One shard = one rank's
+// slab of the frame plus the filter handle (vip.h row-band form) that filters it, a
+// communication stream and two events. A run overlaps the halo exchange (RCCL
+// ncclSend/ncclRecv with the two row neighbours, in one group; or device copies for the
+// LOCAL transport) with the interior rows, whose windows stay inside the own rows, and
+// filters the two r-row edge bands once the halos are in.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <new>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "vip_shard.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int comm_fail(ncclResult_t r, const char* what) {
+    g_last_error = std::string(what) + ": " + ncclGetErrorString(r);
+    return VIP_ERR_COMM;
+}
+
+#define VIP_HIP_TRY(expr)                                 \
+    do {                                                  \
+        const hipError_t e_ = (expr);                     \
+        if (e_ != hipSuccess) return (int)e_;             \
+    } while (0)
+
+// Polls a non-blocking communicator until its pending operation (initialisation or
+// the enqueue of a group) completes, fails, or the deadline passes.
+int wait_comm(ncclComm_t c, int timeout_ms, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(c, &st);
+        if (r != ncclSuccess) return comm_fail(r, what);
+        if (st == ncclSuccess) return 0;
+        if (st != ncclInProgress) return comm_fail(st, what);
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
+        if (ms.count() > timeout_ms) {
+            g_last_error = std::string(what) + ": not complete after " + std::to_string(timeout_ms) + " ms";
+            return VIP_ERR_COMM_TIMEOUT;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
+int default_timeout(int t) { return t > 0 ? t : 180000; }
+
+}  // namespace
+
+struct vip_shard_s {
+    int kind, width, frame_height, ksize, numerics;
+    int nranks, rank, transport, device, timeout_ms;
+    int row_begin, own, r;
+    vip_bilateral_t bil = nullptr;
+    vip_adaptive_t ada = nullptr;
+    hipStream_t comm = nullptr;  // halo exchange stream
+    hipEvent_t ev_in = nullptr;  // own rows written (on the caller's stream)
+    hipEvent_t ev_x = nullptr;   // halos received (on comm)
+    ncclComm_t nccl = nullptr;   // VIP_SHARD_RCCL
+    bool above() const { return rank > 0 && r > 0; }
+    bool below() const { return rank < nranks - 1 && r > 0; }
+    int slab_rows() const { return own + 2 * r; }
+    size_t pitch() const { return (size_t)width * 3; }
+};
+
+extern "C" int vip_shard_destroy(vip_shard_t h);
+
+namespace {
+
+// Filter handle, stream and events of a shard on the current device (geometry set).
+int init_shard(vip_shard_s* h, float sigma_space, float sigma_color) {
+    VIP_HIP_TRY(hipGetDevice(&h->device));
+    int rc = h->kind == VIP_FILTER_ADAPTIVE
+                 ? vip_adaptive_create(&h->ada, h->width, h->slab_rows(), h->ksize, sigma_space, sigma_color,
+                                       h->numerics)
+                 : vip_bilateral_create(&h->bil, h->width, h->slab_rows(), h->ksize, sigma_space, sigma_color,
+                                        h->numerics);
+    if (rc) return rc;
+    VIP_HIP_TRY(hipStreamCreateWithFlags(&h->comm, hipStreamNonBlocking));
+    VIP_HIP_TRY(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
+    VIP_HIP_TRY(hipEventCreateWithFlags(&h->ev_x, hipEventDisableTiming));
+    return 0;
+}
+
+// Geometry shared by every rank (sharded.py SlabGeometry); VIP_ERR_INVALID_ARGUMENT when
+// the thinnest shard cannot cover a halo (checked identically on every rank, before any
+// communication, so no rank is left waiting in an exchange the others never join).
+int new_shard(vip_shard_s** out, int kind, int width, int frame_height, int ksize, int numerics, int nranks, int rank,
+              int transport, int timeout_ms) {
+    if (!out || width <= 0 || frame_height <= 0 || nranks <= 0 || rank < 0 || rank >= nranks)
+        return VIP_ERR_INVALID_ARGUMENT;
+    if (kind != VIP_FILTER_BILATERAL && kind != VIP_FILTER_ADAPTIVE) return VIP_ERR_INVALID_ARGUMENT;
+    if (ksize < 1 || !(ksize & 1)) return VIP_ERR_UNSUPPORTED_KSIZE;
+    const int r = ksize / 2;
+    if (nranks > 1 && frame_height / nranks < r) return VIP_ERR_INVALID_ARGUMENT;
+    auto* h = new (std::nothrow) vip_shard_s();
+    if (!h) return (int)hipErrorOutOfMemory;
+    h->kind = kind;
+    h->width = width;
+    h->frame_height = frame_height;
+    h->ksize = ksize;
+    h->numerics = numerics;
+    h->nranks = nranks;
+    h->rank = rank;
+    h->transport = transport;
+    h->timeout_ms = default_timeout(timeout_ms);
+    vip_shard_rows(frame_height, nranks, rank, &h->row_begin, &h->own);
+    h->r = r;
+    *out = h;
+    return 0;
+}
+
+// Rows the shard's filter may read: the halos where a neighbour supplies them, else the
+// own rows (the reference's replicate border at the frame's top and bottom).
+void clamp_range(const vip_shard_s* h, int* lo, int* hi) {
+    *lo = h->above() ? 0 : h->r;
+    *hi = h->below() ? h->slab_rows() : h->r + h->own;
+}
+
+// Own rows [row0, row0 + n) of the slab -> the same rows of out.
+int filter_rows(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pitch, int row0, int n,
+                hipStream_t s) {
+    if (n <= 0) return 0;
+    int lo, hi;
+    clamp_range(h, &lo, &hi);
+    uint8_t* o = out + (size_t)row0 * out_pitch;
+    if (h->kind == VIP_FILTER_ADAPTIVE)
+        return vip_adaptive_run_rows(h->ada, slab, h->pitch(), o, out_pitch, n, h->r + row0, lo, hi, s);
+    return vip_bilateral_run_rows(h->bil, slab, h->pitch(), nullptr, 0, o, out_pitch, n, h->r + row0, lo, hi, s);
+}
+
+// Interior rows [r, own - r) read only own rows; the edge bands need the halos.
+int interior(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pitch, hipStream_t s) {
+    return filter_rows(h, slab, out, out_pitch, h->r, h->own - 2 * h->r, s);
+}
+int edges(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pitch, hipStream_t s) {
+    const int top = h->r < h->own ? h->r : h->own;
+    const int b0 = h->own - h->r > top ? h->own - h->r : top;
+    int rc = filter_rows(h, slab, out, out_pitch, 0, top, s);
+    if (!rc) rc = filter_rows(h, slab, out, out_pitch, b0, h->own - b0, s);
+    return rc;
+}
+
+// This shard's sends and receives (inside the caller's ncclGroupStart/End).
+int enqueue_p2p(const vip_shard_s* h, uint8_t* slab) {
+    const size_t bytes = (size_t)h->r * h->pitch();
+    ncclResult_t e = ncclSuccess;
+    if (h->above()) {
+        if ((e = ncclSend(slab + (size_t)h->r * h->pitch(), bytes, ncclUint8, h->rank - 1, h->nccl, h->comm)))
+            return comm_fail(e, "ncclSend (up)");
+        if ((e = ncclRecv(slab, bytes, ncclUint8, h->rank - 1, h->nccl, h->comm))) return comm_fail(e, "ncclRecv (up)");
+    }
+    if (h->below()) {
+        if ((e = ncclSend(slab + (size_t)h->own * h->pitch(), bytes, ncclUint8, h->rank + 1, h->nccl, h->comm)))
+            return comm_fail(e, "ncclSend (down)");
+        if ((e = ncclRecv(slab + (size_t)(h->r + h->own) * h->pitch(), bytes, ncclUint8, h->rank + 1, h->nccl, h->comm)))
+            return comm_fail(e, "ncclRecv (down)");
+    }
+    return 0;
+}
+
+int group_end(vip_shard_s* const* hs, int n) {
+    const ncclResult_t e = ncclGroupEnd();
+    if (e != ncclSuccess && e != ncclInProgress) return comm_fail(e, "ncclGroupEnd");
+    for (int i = 0; i < n; ++i)
+        if (const int rc = wait_comm(hs[i]->nccl, hs[i]->timeout_ms, "halo exchange")) return rc;
+    return 0;
+}
+
+// Record `ev` on `s` when the caller asked for timing events.
+int mark(void* const* events, int k, hipStream_t s) {
+    return events ? (int)hipEventRecord((hipEvent_t)events[k], s) : 0;
+}
+
+struct DeviceGuard {  // restores the caller's current device
+    int dev = -1;
+    DeviceGuard() { (void)hipGetDevice(&dev); }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int vip_shard_rows(int frame_height, int nranks, int rank, int* row_begin, int* own_rows) {
+    if (frame_height < 0 || nranks <= 0 || rank < 0 || rank >= nranks || !row_begin || !own_rows)
+        return VIP_ERR_INVALID_ARGUMENT;
+    const int base = frame_height / nranks, rem = frame_height % nranks;
+    *row_begin = rank * base + (rank < rem ? rank : rem);
+    *own_rows = base + (rank < rem ? 1 : 0);
+    return 0;
+}
+
+int vip_shard_unique_id(void* id) {
+    if (!id) return VIP_ERR_INVALID_ARGUMENT;
+    static_assert(sizeof(ncclUniqueId) == VIP_SHARD_ID_BYTES, "id size");
+    ncclUniqueId u;
+    if (const ncclResult_t e = ncclGetUniqueId(&u)) return comm_fail(e, "ncclGetUniqueId");
+    std::memcpy(id, &u, sizeof(u));
+    return 0;
+}
+
+const char* vip_shard_last_error(void) { return g_last_error.c_str(); }
+
+int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
+                     float sigma_color, int numerics, int nranks, int rank, const void* id, int timeout_ms) {
+    if (!out || !id) return VIP_ERR_INVALID_ARGUMENT;
+    vip_shard_s* h = nullptr;
+    int rc = new_shard(&h, kind, width, frame_height, ksize, numerics, nranks, rank, VIP_SHARD_RCCL, timeout_ms);
+    if (rc) return rc;
+    rc = init_shard(h, sigma_space, sigma_color);
+    if (!rc) {
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;  // poll with a deadline instead of blocking for a missing rank
+        const ncclResult_t e = ncclCommInitRankConfig(&h->nccl, nranks, u, rank, &cfg);
+        if (e != ncclSuccess && e != ncclInProgress) rc = comm_fail(e, "ncclCommInitRankConfig");
+        if (!rc && h->nccl) rc = wait_comm(h->nccl, h->timeout_ms, "communicator initialisation");
+    }
+    if (rc) {
+        vip_shard_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* devices, int kind, int width,
+                           int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
+                           int timeout_ms) {
+    if (!out || n <= 0 || (transport != VIP_SHARD_RCCL && transport != VIP_SHARD_LOCAL)) return VIP_ERR_INVALID_ARGUMENT;
+    if (transport == VIP_SHARD_RCCL && !devices) return VIP_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard;
+    for (int i = 0; i < n; ++i) out[i] = nullptr;
+    int rc = 0;
+    for (int i = 0; i < n && !rc; ++i) {
+        rc = new_shard(&out[i], kind, width, frame_height, ksize, numerics, n, i, transport, timeout_ms);
+        if (!rc && transport == VIP_SHARD_RCCL) rc = (int)hipSetDevice(devices[i]);
+        if (!rc) rc = init_shard(out[i], sigma_space, sigma_color);
+    }
+    if (!rc && transport == VIP_SHARD_RCCL) {
+        // one communicator per device, initialised in one group (ncclCommInitAll's pattern)
+        ncclUniqueId u;
+        ncclResult_t e = ncclGetUniqueId(&u);
+        if (e) rc = comm_fail(e, "ncclGetUniqueId");
+        if (!rc && (e = ncclGroupStart())) rc = comm_fail(e, "ncclGroupStart");
+        for (int i = 0; i < n && !rc; ++i) {
+            rc = (int)hipSetDevice(devices[i]);
+            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+            cfg.blocking = 0;
+            if (!rc && (e = ncclCommInitRankConfig(&out[i]->nccl, n, u, i, &cfg)) && e != ncclInProgress)
+                rc = comm_fail(e, "ncclCommInitRankConfig");
+        }
+        e = ncclGroupEnd();
+        if (!rc && e != ncclSuccess && e != ncclInProgress) rc = comm_fail(e, "ncclGroupEnd (init)");
+        for (int i = 0; i < n && !rc; ++i) rc = wait_comm(out[i]->nccl, out[i]->timeout_ms, "communicator initialisation");
+    }
+    if (rc) {
+        for (int i = 0; i < n; ++i) {
+            vip_shard_destroy(out[i]);
+            out[i] = nullptr;
+        }
+    }
+    return rc;
+}
+
+int vip_shard_geometry(vip_shard_t h, int* row_begin, int* own_rows, int* halo_rows) {
+    if (!h || !row_begin || !own_rows || !halo_rows) return VIP_ERR_INVALID_ARGUMENT;
+    *row_begin = h->row_begin;
+    *own_rows = h->own;
+    *halo_rows = h->r;
+    return 0;
+}
+
+static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitch, void* stream,
+                     void* const* events) {
+    if (!h || !slab || !out || out_pitch < h->pitch() || h->transport != VIP_SHARD_RCCL || !h->nccl)
+        return VIP_ERR_INVALID_ARGUMENT;
+    const hipStream_t s = (hipStream_t)stream;
+    VIP_HIP_TRY(hipSetDevice(h->device));
+    int rc = mark(events, 0, s);
+    if (!rc && !h->above() && !h->below()) {  // no neighbours: one launch over the own rows
+        rc = mark(events, 1, s);
+        if (!rc) rc = filter_rows(h, slab, out, out_pitch, 0, h->own, s);
+        if (!rc) rc = mark(events, 2, s);
+        if (!rc) rc = mark(events, 3, s);
+        return rc;
+    }
+    // exchange first on the communication stream (its kernel is dispatched ahead of the
+    // interior launch), then the interior on the caller's stream, then the edges after
+    // the halos
+    if (!rc) rc = (int)hipEventRecord(h->ev_in, s);
+    if (!rc) rc = (int)hipStreamWaitEvent(h->comm, h->ev_in, 0);
+    if (!rc) {
+        if (const ncclResult_t e = ncclGroupStart()) rc = comm_fail(e, "ncclGroupStart");
+        if (!rc) rc = enqueue_p2p(h, slab);
+        const int rc2 = group_end(&h, 1);
+        if (!rc) rc = rc2;
+    }
+    if (!rc) rc = mark(events, 1, h->comm);
+    if (!rc) rc = (int)hipEventRecord(h->ev_x, h->comm);
+    if (!rc) rc = interior(h, slab, out, out_pitch, s);
+    if (!rc) rc = mark(events, 2, s);
+    if (!rc) rc = (int)hipStreamWaitEvent(s, h->ev_x, 0);
+    if (!rc) rc = edges(h, slab, out, out_pitch, s);
+    if (!rc) rc = mark(events, 3, s);
+    return rc;
+}
+
+int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream) {
+    DeviceGuard guard;
+    return shard_run(h, d_slab, d_out, out_pitch, stream, nullptr);
+}
+
+int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream,
+                        void* const* events) {
+    if (!events) return VIP_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard;
+    return shard_run(h, d_slab, d_out, out_pitch, stream, events);
+}
+
+int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* const* outs, size_t out_pitch,
+                        void* const* streams) {
+    if (!hs || n <= 0 || !slabs || !outs || !streams) return VIP_ERR_INVALID_ARGUMENT;
+    for (int i = 0; i < n; ++i)
+        if (!hs[i] || hs[i]->nranks != n || hs[i]->rank != i || hs[i]->transport != hs[0]->transport ||
+            !slabs[i] || !outs[i] || out_pitch < hs[i]->pitch())
+            return VIP_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard;
+    const bool rccl = hs[0]->transport == VIP_SHARD_RCCL;
+    auto st = [&](int i) { return (hipStream_t)streams[i]; };
+    // own rows written -> the exchange may read them
+    for (int i = 0; i < n; ++i) {
+        VIP_HIP_TRY(hipSetDevice(hs[i]->device));
+        VIP_HIP_TRY(hipEventRecord(hs[i]->ev_in, st(i)));
+    }
+    if (n > 1 && hs[0]->r > 0) {
+        if (rccl) {
+            for (int i = 0; i < n; ++i) {
+                VIP_HIP_TRY(hipSetDevice(hs[i]->device));
+                VIP_HIP_TRY(hipStreamWaitEvent(hs[i]->comm, hs[i]->ev_in, 0));
+            }
+            if (const ncclResult_t e = ncclGroupStart()) return comm_fail(e, "ncclGroupStart");
+            int rc = 0;
+            for (int i = 0; i < n && !rc; ++i) {
+                rc = (int)hipSetDevice(hs[i]->device);
+                if (!rc) rc = enqueue_p2p(hs[i], slabs[i]);
+            }
+            const int rc2 = group_end(hs, n);
+            if (rc || rc2) return rc ? rc : rc2;
+            for (int i = 0; i < n; ++i) {
+                VIP_HIP_TRY(hipSetDevice(hs[i]->device));
+                VIP_HIP_TRY(hipEventRecord(hs[i]->ev_x, hs[i]->comm));
+            }
+        } else {
+            // LOCAL: every slab on one device; shard 0's stream carries all the copies
+            const hipStream_t c = hs[0]->comm;
+            for (int i = 0; i < n; ++i) VIP_HIP_TRY(hipStreamWaitEvent(c, hs[i]->ev_in, 0));
+            for (int i = 0; i < n; ++i) {
+                const vip_shard_s* h = hs[i];
+                const size_t bytes = (size_t)h->r * h->pitch();
+                if (i > 0)  // own top rows -> the halo below of shard i - 1
+                    VIP_HIP_TRY(hipMemcpyAsync(slabs[i - 1] + (size_t)(hs[i - 1]->r + hs[i - 1]->own) * h->pitch(),
+                                               slabs[i] + (size_t)h->r * h->pitch(), bytes, hipMemcpyDeviceToDevice, c));
+                if (i < n - 1)  // own bottom rows -> the halo above of shard i + 1
+                    VIP_HIP_TRY(hipMemcpyAsync(slabs[i + 1], slabs[i] + (size_t)h->own * h->pitch(), bytes,
+                                               hipMemcpyDeviceToDevice, c));
+            }
+            VIP_HIP_TRY(hipEventRecord(hs[0]->ev_x, c));  // shard 0's event covers the group
+        }
+        for (int i = 0; i < n; ++i) {
+            VIP_HIP_TRY(hipSetDevice(hs[i]->device));
+            if (const int rc = interior(hs[i], slabs[i], outs[i], out_pitch, st(i))) return rc;
+            VIP_HIP_TRY(hipStreamWaitEvent(st(i), rccl ? hs[i]->ev_x : hs[0]->ev_x, 0));
+            if (const int rc = edges(hs[i], slabs[i], outs[i], out_pitch, st(i))) return rc;
+        }
+        return 0;
+    }
+    for (int i = 0; i < n; ++i) {  // one shard or no halo: nothing to exchange
+        VIP_HIP_TRY(hipSetDevice(hs[i]->device));
+        if (const int rc = filter_rows(hs[i], slabs[i], outs[i], out_pitch, 0, hs[i]->own, st(i))) return rc;
+    }
+    return 0;
+}
+
+int vip_shard_destroy(vip_shard_t h) {
+    if (!h) return 0;
+    DeviceGuard guard;
+    (void)hipSetDevice(h->device);
+    if (h->nccl) {
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(h->nccl, &st) == ncclSuccess && st == ncclSuccess)
+            (void)ncclCommDestroy(h->nccl);
+        else
+            (void)ncclCommAbort(h->nccl);  // an initialisation that timed out or failed
+    }
+    if (h->bil) vip_bilateral_destroy(h->bil);
+    if (h->ada) vip_adaptive_destroy(h->ada);
+    if (h->comm) (void)hipStreamDestroy(h->comm);
+    if (h->ev_in) (void)hipEventDestroy(h->ev_in);
+    if (h->ev_x) (void)hipEventDestroy(h->ev_x);
+    delete h;
+    return 0;
+}
+
+}  // extern "C"

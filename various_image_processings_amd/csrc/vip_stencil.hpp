@@ -516,7 +516,7 @@ __device__ __forceinline__ uint32_t pack_u8_clamped(float v, uint32_t sel, uint3
     return __builtin_amdgcn_cvt_pk_u8_f32(__builtin_floorf(v), sel, word);
 }
 
-// RN(1/k) for k in [1, 2^17): hardware rcp (1 ulp) + one Newton step. Verified
+// RN(1/k) for k in [1, 2^38): hardware rcp (1 ulp) + one Newton step. Verified
 // exhaustively over every float of that range by microbench/div_check.hip.
 __device__ __forceinline__ float recip_exact(float k) {
     const float y0 = __builtin_amdgcn_rcpf(k);

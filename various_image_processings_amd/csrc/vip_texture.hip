@@ -751,8 +751,10 @@ VIP_GF_STAMP(8);
             // on the GPU; microbench/exp_check against glibc, the oracle's exp)
             const float e = exp_tab_f32(arg, etab);
 #endif
-            // 2 / (1 + e) == 2 * RN(1 / (1 + e)) exactly (a power-of-two scale); e >= 1, so
-            // recip_exact's argument is in [2, 2^17) here, where div_check verifies it
+            // 2 / (1 + e) == 2 * RN(1 / (1 + e)) exactly (a power-of-two scale). e >= 1 and
+            // arg <= 255 / (5 ksize) (rtv <= 255): 1 + e < 2^17 for ksize >= 5, < 2^37 at
+            // ksize 2 (ksize 1: arg = 0). microbench/div_check verifies recip_exact for every
+            // float in [1, 2^38)
             const float alpha = 2.f * recip_exact(1.f + e) - 1.f;
             const float beta = 1.f - alpha;
             uint32_t gw = 0;

@@ -219,3 +219,117 @@ class ShardedTexture:
                 b = self._scratch[t % 2]
                 self.impl.iterate_rows(a, b[r0:r1], r0, r1 - r0, lo, hi, stream=stream)
                 a = b
+
+
+# ---------------------------------------------------------------------------
+# Native path: include/vip_shard.h (libvip_shard.so). The exchange runs in C++ over the
+# library's own RCCL communicator (ncclSend/ncclRecv with the row neighbours), enqueued
+# on a communication stream together with the interior rows on the filter stream; the
+# two r-row edge bands follow once the halos are in. Same SlabGeometry, same results.
+# ---------------------------------------------------------------------------
+def _shard_kind(adaptive: bool) -> int:
+    from . import _lib
+    return _lib.VIP_FILTER_ADAPTIVE if adaptive else _lib.VIP_FILTER_BILATERAL
+
+
+def native_unique_id() -> bytes:
+    """The communicator id (ncclGetUniqueId) rank 0 creates and broadcasts."""
+    import ctypes
+    from . import _shard_lib as S
+    buf = ctypes.create_string_buffer(S.VIP_SHARD_ID_BYTES)
+    S.call("vip_shard_unique_id", buf)
+    return buf.raw
+
+
+def native_rows(frame_height: int, world: int, rank: int) -> tuple[int, int]:
+    """vip_shard_rows: (first row, own rows), == shard_rows (no device call)."""
+    import ctypes
+    from . import _shard_lib as S
+    b, n = ctypes.c_int(), ctypes.c_int()
+    S.call("vip_shard_rows", frame_height, world, rank, ctypes.byref(b), ctypes.byref(n))
+    return b.value, b.value + n.value
+
+
+class NativeShard:
+    """This rank's shard of a row-sharded frame (one process per GPU, RCCL transport)."""
+
+    def __init__(self, width: int, frame_height: int, ksize: int, rank: int, world: int, unique_id: bytes,
+                 sigma_space: float = 10.0, sigma_color: float = 30.0, adaptive: bool = False, numerics: int = 0,
+                 timeout_ms: int = 180000):
+        import ctypes
+        from . import _shard_lib as S
+        self._h = ctypes.c_void_p()
+        idb = ctypes.create_string_buffer(bytes(unique_id), S.VIP_SHARD_ID_BYTES)
+        S.call("vip_shard_create", ctypes.byref(self._h), _shard_kind(adaptive), width, frame_height, ksize,
+               sigma_space, sigma_color, numerics, world, rank, idb, int(timeout_ms))
+        self.geo = SlabGeometry(width, frame_height, ksize // 2, rank, world)
+
+    def filter(self, slab, out, stream=None) -> None:
+        """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3). Asynchronous."""
+        from . import _shard_lib as S
+        from .filters import _ptr, _stream
+        p = self.geo.width * 3
+        S.call("vip_shard_run", self._h, _ptr(slab, p * self.geo.slab_rows), _ptr(out, p * self.geo.own), p,
+               _stream(stream))
+
+    def filter_timed(self, slab, out, events, stream=None) -> None:
+        """events: 4 timing-enabled torch.cuda.Event (vip_shard_run_timed): run start,
+        halos received (communication stream), interior done, edges done."""
+        import ctypes
+        from . import _shard_lib as S
+        from .filters import _ptr, _stream
+        for e in events:
+            e.record()  # materialise the hipEvent_t behind the torch event
+        arr = (ctypes.c_void_p * 4)(*[e.cuda_event for e in events])
+        p = self.geo.width * 3
+        S.call("vip_shard_run_timed", self._h, _ptr(slab, p * self.geo.slab_rows), _ptr(out, p * self.geo.own), p,
+               _stream(stream), arr)
+
+    def __del__(self):
+        try:
+            if self._h and self._h.value:
+                from . import _shard_lib as S
+                S.lib().vip_shard_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class ShardGroup:
+    """All shards of a frame in ONE process: transport LOCAL (every slab on the current
+    device, halos by device copies -- the native exchange path on one GPU) or RCCL over
+    `devices` (one communicator per device, ncclCommInitAll's pattern)."""
+
+    def __init__(self, n: int, width: int, frame_height: int, ksize: int, transport: int = 1, devices=None,
+                 sigma_space: float = 10.0, sigma_color: float = 30.0, adaptive: bool = False, numerics: int = 0,
+                 timeout_ms: int = 180000):
+        import ctypes
+        from . import _shard_lib as S
+        self.n = n
+        self._hs = (ctypes.c_void_p * n)()
+        devs = None if devices is None else (ctypes.c_int * n)(*devices)
+        S.call("vip_shard_create_group", self._hs, n, transport, devs, _shard_kind(adaptive), width, frame_height,
+               ksize, sigma_space, sigma_color, numerics, int(timeout_ms))
+        self.geos = [SlabGeometry(width, frame_height, ksize // 2, i, n) for i in range(n)]
+
+    def filter(self, slabs, outs, streams) -> None:
+        import ctypes
+        from . import _shard_lib as S
+        from .filters import _ptr, _stream
+        n = self.n
+        g = self.geos
+        p = g[0].width * 3
+        sl = (ctypes.c_void_p * n)(*[_ptr(s, p * g[i].slab_rows) for i, s in enumerate(slabs)])
+        ou = (ctypes.c_void_p * n)(*[_ptr(o, p * g[i].own) for i, o in enumerate(outs)])
+        st = (ctypes.c_void_p * n)(*[_stream(s) for s in streams])
+        S.call("vip_shard_run_group", self._hs, n, sl, ou, p, st)
+
+    def __del__(self):
+        try:
+            from . import _shard_lib as S
+            for i in range(self.n):
+                if self._hs[i]:
+                    S.lib().vip_shard_destroy(self._hs[i])
+                    self._hs[i] = None
+        except Exception:
+            pass
