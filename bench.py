@@ -6,12 +6,15 @@
 
 One step = one filter application over each rank's row slab of a frame that is
 row-sharded across the N GPUs (one process per GPU, torch.distributed over
-RCCL/xGMI; N>1 is launched by torch.distributed.run). Before each step's kernel
-the ranks exchange their r-row halos (sendrecv with the row neighbours only).
+RCCL/xGMI; N>1 is launched by torch.distributed.run). Each step the ranks exchange
+their r-row halos with the row neighbours only (include/vip_shard.h: ncclSend/ncclRecv
+on the library's own RCCL communicator, overlapped with the interior rows, whose
+windows need no halo; the edge bands follow).
 
-  c2 (default) bilateral r=7 (ksize 15, sigma_space 10, sigma_color 30); each rank
-     owns a full 3840x2160 RGB8 frame's worth of rows of an (N*2160)x3840 frame
-     -> weak scaling; at N=1 this is exactly BASELINE config 2.
+  c2 (default) bilateral r=7 (ksize 15, sigma_space 10, sigma_color 30) on the
+     3840x2160 RGB8 frame, its rows split over the N ranks (strong scaling: BASELINE
+     config 2 at every N); the line also reports the weak-scaling figure (a 2160-row
+     slab per rank of an (N*2160)x3840 frame) under "weak".
   c3 adaptive bilateral r=7, same geometry (BASELINE config 3).
   c4 bilateral texture filter k=5, nitr=5 on 3840x2160 per rank (BASELINE config
      4); N>1 row-shards an (N*2160)x3840 frame with one 45-row halo exchange per
@@ -91,7 +94,8 @@ def parse():
     p.add_argument("--same-device", action="store_true")
     # SURVEY 8(d) inputs: (i) uniform 0..254 like test/random_array.hpp (default), (ii) narrow
     # uniform [100, 120) like sample/benchmark/main.cpp:213, (iii) lenna tiled to the frame
-    p.add_argument("--data", default="uniform", choices=["uniform", "narrow", "lenna"])
+    p.add_argument("--data", default=None, choices=["uniform", "narrow", "lenna"],
+                   help="input statistics (default: the config's own -- lenna for c1, uniform otherwise)")
     # the reference's sample/benchmark table instead of the contract line
     p.add_argument("--sample-table", action="store_true")
     p.add_argument("--sample-size", default="100x100")
@@ -104,6 +108,17 @@ def parse():
     # 0.178 -> 0.173 ms, C3 0.327 -> 0.323, C4 0.717 -> 0.641 ms per frame with 2; 3 no
     # better. S must divide the 12 rotating buffers (a buffer always meets the same stream)
     p.add_argument("--streams", type=int, default=2, choices=[1, 2, 3, 4, 6])
+    # N>1: "strong" splits the metric's frame (C2/C3: 3840x2160) over the ranks (default
+    # for c2, c3, c5), "weak" gives every rank a 2160-row slab of an (N*2160)-row frame
+    # (default for c4). A strong c2/c3 line also carries the weak figure ("weak" key)
+    # unless --no-weak.
+    p.add_argument("--scaling", default=None, choices=["strong", "weak"])
+    p.add_argument("--no-weak", action="store_true")
+    # N>1 halo exchange: "native" = include/vip_shard.h (C++ over the library's own RCCL
+    # communicator, overlapped with the interior rows; torch.distributed/gloo only for
+    # control), "torch" = torch.distributed P2P before the kernel. Default native, torch for
+    # the one-GPU gloo rehearsal and the texture filter.
+    p.add_argument("--exchange", default=None, choices=["native", "torch"])
     return p.parse_args()
 
 
@@ -351,63 +366,73 @@ def sample_table(args) -> None:
         print(f"{name + ' [hip]':40s} : {measure(hip):10.6f} [msec]")
 
 
-def main():
-    args = parse()
-    if args.sample_table:
-        sample_table(args)
-        return
+def init_distributed(args, rank, dev):
+    """Process group for N>1. With the native exchange (include/vip_shard.h) the halos
+    move over the library's own RCCL communicator and torch.distributed only carries the
+    control traffic (the communicator id, barriers, the max over ranks): gloo. Otherwise
+    the halos move through torch.distributed P2P: nccl (= RCCL), or gloo for the one-GPU
+    rehearsal. A rank that cannot join ends the run with a message and status 3, never a
+    hang: bounded rendezvous and collective timeouts."""
+    import datetime
+
+    import torch.distributed as dist
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    backend = "gloo" if args.exchange == "native" else args.backend
+    try:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=180))
+        else:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=180))
+        dist.barrier()  # communicator up before the first halo exchange
+    except Exception as e:  # noqa: BLE001
+        print(f"bench.py rank {rank}: process group ({backend}) failed: {e!r}", file=sys.stderr, flush=True)
+        os._exit(3)
+    return backend
+
+
+def native_shard(args, cfg, frame_h, rank, world):
+    """This rank's NativeShard (vip_shard_create over a communicator id from rank 0),
+    or (None, reason) when any rank failed to create it -- all ranks agree (gloo)."""
     import torch
     import torch.distributed as dist
 
-    cfg = CONFIGS[args.config]
-    if args.steps is None:
-        args.steps = DEFAULT_STEPS[args.config]
-    if "data" in cfg and args.data == "uniform":
-        args.data = cfg["data"]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    if args.same_device:
-        local = 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        # a rank that cannot join (RCCL init failure, a missing peer) must end the run
-        # with a message and a non-zero status, never hang: bounded rendezvous and
-        # collective timeouts (the NCCL watchdog aborts a stuck P2P after `timeout`)
-        import datetime
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-        try:
-            if args.backend == "nccl":
-                dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=180))
-            else:
-                dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=180))
-            dist.barrier()  # communicator up before the first (P2P) halo exchange
-        except Exception as e:  # noqa: BLE001
-            print(f"bench.py rank {rank}: process group ({args.backend}) failed: {e!r}", file=sys.stderr, flush=True)
-            os._exit(3)
+    from various_image_processings_amd.sharded import NativeShard, native_unique_id
+    box = [native_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    ns, err = None, ""
+    try:
+        ns = NativeShard(cfg["width"], frame_h, cfg["ksize"], rank, world, box[0], adaptive=cfg["kind"] == "adaptive",
+                         timeout_ms=120000)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {rank}: {e}"
+        print(f"bench.py {err}", file=sys.stderr, flush=True)
+    ok = torch.tensor([0 if ns is None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok[0]) == 0:
+        return None, err or "another rank failed to create its shard"
+    return ns, None
 
-    import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
+
+def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
+    """Build one workload (buffers, handles) and time it: W warm-up steps, then K steps
+    between barriers + device syncs, max over ranks. Returns the measured quantities."""
+    import torch.distributed as dist
+
     from various_image_processings_amd.filters import _TextureImpl
     from various_image_processings_amd.sharded import ShardedBilateral, ShardedTexture, exchange_halo
 
-    S = args.streams
-    # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    S = len(streams)
     stream = streams[0]
     sraw = [st.cuda_stream for st in streams]  # hipStream_t of each stream
-    w = cfg["width"]
-    k = cfg["ksize"]
-    r = k // 2
+    w, k = cfg["width"], cfg["ksize"]
     gen = torch.Generator(device=dev)
     gen.manual_seed(42 + rank)
+    res = dict(frame_h=frame_h, exchange=None, stage_ms=None, samples=None)
+    native = False
+    cdev = dev if state.get("backend") == "nccl" else "cpu"  # control tensors of the process group
 
     if cfg["kind"] == "texture" and world == 1:
-        rows = cfg["rows_per_rank"]
-        frame_h = rows
+        rows = frame_h
         geo = None
         # one handle per stream: a texture handle owns its ping-pong and guide frames
         texs = [_TextureImpl(w, rows, k, cfg["nitr"]) for _ in range(S)]
@@ -417,7 +442,6 @@ def main():
         srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         smarks = []
-
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
 
         def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
@@ -432,7 +456,6 @@ def main():
         # row-sharded frame: one halo exchange of nitr * texture_halo_rows(k) rows per
         # frame, then shrinking ghost zones (sharded.ShardedTexture; one per stream: it
         # owns scratch slabs)
-        frame_h = cfg["rows_per_rank"] * world
         sts = [ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world) for _ in range(S)]
         geo = sts[0].geo
         rows = geo.own
@@ -442,39 +465,60 @@ def main():
         def run(i, s=stream, h=0):
             sts[h].filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
     else:
-        frame_h = cfg.get("frame_height", cfg.get("rows_per_rank", 0) * world)
+        ns = None
+        if world > 1 and args.exchange == "native":
+            ns, why = native_shard(args, cfg, frame_h, rank, world)
+            if ns is None:  # fall back to torch.distributed P2P over a new RCCL group
+                if "torch_group" not in state:
+                    state["torch_group"] = dist.new_group(backend="nccl" if args.backend == "nccl" else "gloo")
+                res["exchange_fallback"] = why
+        native = ns is not None
         # the handle holds only read-only LUTs: one serves every stream
-        sb = ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
+        sb = ns if native else ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
         geo = sb.geo
         rows = geo.own
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
-
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
-
-        def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
-            sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h], exchange=False)
+        if native:
+            def run(i, s=stream, h=0):  # exchange + interior + edges (vip_shard_run)
+                sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h])
+        else:
+            def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
+                sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h], exchange=False)
+    res["exchange"] = (None if world == 1 else
+                       "native vip_shard (RCCL ncclSend/ncclRecv, overlapped with the interior rows)" if native else
+                       f"torch.distributed P2P ({state.get('backend', args.backend)}), serial before the kernel")
 
     # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time per frame
     # (with S > 1 streams: per frame with S frames in flight).
-    # N>1: the halo exchange sits between kernels; the timed steps carry no inner events
-    # (an event between launches costs stream time, ~11 us per pair measured with
-    # rocprofv3), so max(4, K/4) further steps after the timed region, on one stream, are
-    # bracketed by events before the exchange, between exchange and kernel(s), and after
-    # them: exchange_ms and kernel_ms per rank.
+    # N>1: the timed steps carry no inner events (an event between launches costs stream
+    # time); max(4, K/4) further steps after the timed region, on one stream, carry them:
+    # torch exchange -- before the exchange, between exchange and kernel, after it;
+    # native -- vip_shard_run_timed's run start, halos in, interior done, edges done.
     marks = []
+    group = state.get("torch_group")
 
     def step(i, sample=False):
         # step i on stream i % S; buffer i % NBUF therefore always meets the same stream
         # (S divides NBUF), so a halo receive into it is ordered after its last reader
         h = 0 if sample else i % S
         s = streams[h]
+        if native:
+            if sample:
+                m = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                with torch.cuda.stream(s):
+                    sb.filter_timed(srcs[i % NBUF], dsts[i % NBUF], m, stream=s)
+                marks.append(m)
+            else:
+                run(i, s, h)
+            return
         with torch.cuda.stream(s):  # RCCL orders its P2P against the current stream
             if sample:
                 m = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 m[0].record(s)
             if world > 1:
-                exchange_halo(srcs[i % NBUF], geo)
+                exchange_halo(srcs[i % NBUF], geo, group)
             if sample:
                 m[1].record(s)
             run(i, s, h)
@@ -483,16 +527,32 @@ def main():
                 marks.append(m)
 
     # clock settle (untimed): steps for --settle-s seconds of wall time, checked every
-    # few steps with a device sync; then the W warm-up steps
+    # few steps with a device sync; then the W warm-up steps. At N>1 every step exchanges
+    # (the ranks must issue the same P2P sequence), so the settle runs a step count
+    # agreed by rank 0.
     t_settle, i_settle = time.perf_counter(), 0
-    while time.perf_counter() - t_settle < args.settle_s:
+    if world == 1:
+        while time.perf_counter() - t_settle < args.settle_s:
+            for _ in range(8):
+                run(i_settle, streams[i_settle % S], i_settle % S)
+                i_settle += 1
+            torch.cuda.synchronize(dev)
+    else:
         for _ in range(8):
-            run(i_settle, streams[i_settle % S], i_settle % S)
+            step(i_settle)
             i_settle += 1
         torch.cuda.synchronize(dev)
-    settle_steps = i_settle
+        per = max(1e-4, (time.perf_counter() - t_settle) / 8)
+        n = torch.tensor([int(args.settle_s / per)], dtype=torch.int64, device=cdev)
+        dist.broadcast(n, src=0)
+        for _ in range(int(n[0])):
+            step(i_settle)
+            i_settle += 1
+        torch.cuda.synchronize(dev)
+    res["settle_steps"] = i_settle
+    base = i_settle
     for i in range(args.warmup):
-        step(i)
+        step(base + i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -503,7 +563,7 @@ def main():
     for s in streams[1:]:
         s.wait_event(ev0)
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(base + args.warmup + i)
     for s in streams[1:]:
         stream.wait_stream(s)
     ev1.record(stream)
@@ -512,14 +572,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    exchange_ms = None
+    after = base + args.warmup + args.steps
     single_ms = None
+    parts = None
     if world > 1:
         for i in range(max(4, args.steps // 4)):
-            step(args.warmup + args.steps + i, sample=True)
+            step(after + i, sample=True)
         torch.cuda.synchronize(dev)
-        exchange_ms = sum(m[0].elapsed_time(m[1]) for m in marks) / len(marks)
-        kernel_ms = sum(m[1].elapsed_time(m[2]) for m in marks) / len(marks)
+        avg = lambda a, b: sum(m[a].elapsed_time(m[b]) for m in marks) / len(marks)  # noqa: E731
+        if native:
+            parts = dict(exchange_ms=avg(0, 1), interior_ms=avg(0, 2), edges_ms=avg(2, 3), run_ms=avg(0, 3))
+            kernel_ms = parts["run_ms"]
+        else:
+            parts = dict(exchange_ms=avg(0, 1), kernel_ms=avg(1, 2))
+            kernel_ms = parts["kernel_ms"]
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
         if S > 1:
@@ -530,12 +596,11 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for i in range(n1):
-                run(args.warmup + args.steps + i)
+                run(after + i)
             e1.record(stream)
             torch.cuda.synchronize(dev)
             single_ms = e0.elapsed_time(e1) / n1
     launch_ms = single_ms if single_ms is not None else kernel_ms
-    stage_ms = None
     fused = cfg["kind"] == "texture" and world == 1 and args.texture_mode == "fused"
     if cfg["kind"] == "texture" and world == 1 and not fused:
         # Per-stage split of the frame: an event between two launches costs a few us of
@@ -544,30 +609,95 @@ def main():
         # timed region, record events around every launch, and their guide : JBF ratio
         # splits the clean frame time of the timed region (stage_ms, per launch).
         for i in range(max(4, args.steps // 4)):
-            run_staged(args.warmup + args.steps + i)
+            run_staged(after + i)
         torch.cuda.synchronize(dev)
         nit = cfg["nitr"]
         guide = sum(m[2 * t].elapsed_time(m[2 * t + 1]) for m in smarks for t in range(nit))
         jbf = sum(m[2 * t + 1].elapsed_time(m[2 * t + 2]) for m in smarks for t in range(nit))
         per = launch_ms / nit
-        stage_ms = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
-                    "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
-    t = torch.tensor([elapsed, launch_ms, exchange_ms or 0.0], dtype=torch.float64,
-                     device=dev if args.backend == "nccl" else "cpu")
+        res["stage_ms"] = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
+                           "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
+    keys = ["elapsed", "launch"] + (sorted(parts) if parts else [])
+    vals = [elapsed, launch_ms] + ([parts[x] for x in sorted(parts)] if parts else [])
+    t = torch.tensor(vals, dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, launch_ms = float(t[0]), float(t[1])
-    exchange_ms = float(t[2]) if world > 1 else None
+    got = dict(zip(keys, (float(v) for v in t)))
+    res.update(elapsed=got["elapsed"], launch_ms=got["launch"], frame_ms=kernel_ms, rows=rows, geo=geo,
+               parts={x: got[x] for x in sorted(parts)} if parts else None, native=native, fused=fused)
+    return res
 
+
+def main():
+    args = parse()
+    if args.sample_table:
+        sample_table(args)
+        return
+    import torch
+    import torch.distributed as dist
+
+    cfg = CONFIGS[args.config]
+    if args.steps is None:
+        args.steps = DEFAULT_STEPS[args.config]
+    if args.data is None:  # the config's own input unless one is asked for
+        args.data = cfg.get("data", "uniform")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    if args.same_device:
+        local = 0
+    if args.exchange is None:
+        # the native RCCL exchange needs one GPU per rank; the one-GPU rehearsal (gloo,
+        # every rank on cuda:0) keeps the torch P2P path
+        args.exchange = "torch" if (args.same_device or args.backend == "gloo") else "native"
+    if cfg["kind"] == "texture":
+        args.exchange = "torch"  # the texture filter's wide halo goes through ShardedTexture
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    state = {}
+    if world > 1:
+        state["backend"] = init_distributed(args, rank, dev)
+
+    import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
+
+    S = args.streams
+    # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench)
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    if args.scaling is None:
+        # the metric's frame (3840x2160; C5 16384^2) split over the ranks; the texture
+        # filter's 45-row ghost halo makes a split 4K frame mostly redundant work, so C4
+        # scales weakly (a 2160-row slab per rank)
+        args.scaling = "weak" if cfg["kind"] == "texture" else "strong"
+    if "frame_height" in cfg:
+        args.scaling = "strong"
+    per_rank = cfg.get("rows_per_rank")
+    frame_h = cfg.get("frame_height") or (per_rank * world if args.scaling == "weak" else per_rank)
+    m = measure(args, cfg, frame_h, torch, dev, rank, world, streams, state)
+    weak = None
+    if world > 1 and args.scaling == "strong" and per_rank and not args.no_weak:
+        # the weak-scaling figure beside it: a full 2160-row slab per rank of an
+        # (N*2160)x3840 frame
+        wm = measure(args, cfg, per_rank * world, torch, dev, rank, world, streams, state)
+        wpx = wm["rows"] * cfg["width"] * world
+        weak = dict(value=round(wpx / (wm["elapsed"] / args.steps) / 1e6, 2),
+                    ms_per_step=round(wm["elapsed"] / args.steps * 1e3, 4), frame=f"{cfg['width']}x{per_rank * world}",
+                    rows_per_rank=wm["rows"], **({k_: round(v, 4) for k_, v in wm["parts"].items()} if wm["parts"] else {}))
+
+    w, k = cfg["width"], cfg["ksize"]
+    r = k // 2
+    elapsed, launch_ms, rows, geo = m["elapsed"], m["launch_ms"], m["rows"], m["geo"]
     px_per_rank = rows * w
-    total_px = px_per_rank * world if cfg["kind"] == "texture" or "rows_per_rank" in cfg else frame_h * w
+    total_px = frame_h * w
     ms_per_step = elapsed / args.steps * 1e3
     value = total_px / (elapsed / args.steps) / 1e6
 
-    if fused:
+    if m["fused"]:
         roof = texture_fused_roofline(cfg, px_per_rank, launch_ms)
     elif cfg["kind"] == "texture":
-        roof = texture_roofline(args.config, cfg, px_per_rank, launch_ms, stage_ms)
+        roof = texture_roofline(args.config, cfg, px_per_rank, launch_ms, m["stage_ms"])
     else:
         taps = circle_taps(r)
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
@@ -585,7 +715,12 @@ def main():
                              bytes_per_px=6))
         if world == 1:  # the committed PMC summaries are whole-frame launches
             roof["valu_issue"] = valu_issue(args.config, f"void vip::{cfg['kind']}_kernel<{r},", launch_ms)
+        else:
+            roof["avg_launch_note"] = ("per-rank device time of one step on one stream: "
+                                       + ("vip_shard_run (exchange overlapped with the interior rows, then the edges)"
+                                          if m["native"] else "the kernel after the serial exchange"))
 
+    parts = m["parts"] or {}
     out = {
         "metric": BASELINE_METRIC if args.config == "c2" else f"Mpixels/sec {cfg['workload']}",
         "value": round(value, 2),
@@ -595,26 +730,28 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if "frame_height" in cfg else "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": DATA_DESC[args.data] + ", resident in HBM; f32 weights/sums",
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
-                   "frame": f"{w}x{frame_h}", "rows_per_rank": rows,
+                   "frame": f"{w}x{frame_h}", "rows_per_rank": rows, "data": args.data,
                    "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
                    **({"texture_mode": args.texture_mode} if cfg["kind"] == "texture" and world == 1 else {}),
-                   **({"backend": args.backend} if world > 1 else {})},
+                   **({"backend": state.get("backend"), "exchange": m["exchange"]} if world > 1 else {}),
+                   **({"exchange_fallback": m["exchange_fallback"]} if m.get("exchange_fallback") else {})},
         "roofline": roof,
-        # per step, max over ranks: the kernel(s) of one frame on one stream and, at N>1,
-        # the halo exchange before them (event-timed on the filter stream in max(4, K/4)
-        # steps after the timed region); the roofline's launch durations come from it
+        # per step, max over ranks: one frame on one stream (N>1: with its exchange),
+        # event-timed in max(4, K/4) steps after the timed region; the roofline's launch
+        # durations come from it
         "kernel_ms": round(launch_ms, 4),
         # frames in flight on S streams (step i on stream i % S); at N=1 and S>1 the
         # timed region's device time per frame, all streams together
         "streams": S,
-        **({"frame_ms_in_flight": round(kernel_ms, 4)} if world == 1 and S > 1 else {}),
-        "settle": {"seconds": args.settle_s, "steps": settle_steps},
-        **({"exchange_ms": round(exchange_ms, 4)} if exchange_ms is not None else {}),
+        **({"frame_ms_in_flight": round(m["frame_ms"], 4)} if world == 1 and S > 1 else {}),
+        "settle": {"seconds": args.settle_s, "steps": m["settle_steps"]},
+        **{k_: round(v, 4) for k_, v in parts.items()},
+        **({"weak": weak} if weak else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

@@ -73,6 +73,12 @@ int vip_upload(void* d_dst, const void* h_src, size_t bytes);   /* blocking H2D 
 int vip_download(void* h_dst, const void* d_src, size_t bytes); /* blocking D2H */
 int vip_device_synchronize(void);
 int vip_stream_synchronize(void* stream);
+/* Device selection for multi-GPU callers (the reference drives the implicit current
+ * device only): every handle, buffer and launch belongs to the calling thread's
+ * current device at the time of the call. */
+int vip_device_count(int* count);
+int vip_set_device(int device);
+int vip_get_device(int* device);
 
 /* ---- host-frame path (the reference's DeviceImage::upload/download,
  *      src/device_image.cu:10-16, copy pageable memory synchronously through thrust).

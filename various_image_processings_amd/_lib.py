@@ -40,6 +40,9 @@ SIGNATURES = {
     "vip_upload": (_c_int, [_c_void_p, _c_void_p, _c_size_t]),
     "vip_download": (_c_int, [_c_void_p, _c_void_p, _c_size_t]),
     "vip_device_synchronize": (_c_int, []),
+    "vip_device_count": (_c_int, [ctypes.POINTER(_c_int)]),
+    "vip_set_device": (_c_int, [_c_int]),
+    "vip_get_device": (_c_int, [ctypes.POINTER(_c_int)]),
     "vip_stream_synchronize": (_c_int, [_c_void_p]),
     "vip_host_alloc": (_c_int, [ctypes.POINTER(_c_void_p), _c_size_t]),
     "vip_host_free": (_c_int, [_c_void_p]),

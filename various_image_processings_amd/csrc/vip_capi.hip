@@ -274,6 +274,15 @@ int vip_download(void* h_dst, const void* d_src, size_t bytes) {
     return (int)hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost);
 }
 int vip_device_synchronize(void) { return (int)hipDeviceSynchronize(); }
+int vip_device_count(int* count) {
+    if (!count) return VIP_ERR_INVALID_ARGUMENT;
+    return (int)hipGetDeviceCount(count);
+}
+int vip_set_device(int device) { return (int)hipSetDevice(device); }
+int vip_get_device(int* device) {
+    if (!device) return VIP_ERR_INVALID_ARGUMENT;
+    return (int)hipGetDevice(device);
+}
 int vip_stream_synchronize(void* stream) { return (int)hipStreamSynchronize((hipStream_t)stream); }
 int vip_host_alloc(void** h_ptr, size_t bytes) {
     if (!h_ptr) return VIP_ERR_INVALID_ARGUMENT;

@@ -10,7 +10,11 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
+#include <memory>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -54,6 +58,44 @@ int wait_comm(ncclComm_t c, int timeout_ms, const char* what) {
 }
 
 int default_timeout(int t) { return t > 0 ? t : 180000; }
+
+// Communicator initialisation, bounded: RCCL's init blocks in its bootstrap until every
+// rank has joined (measured: ncclCommInitRankConfig with blocking = 0 does not return
+// either while a rank is missing), and ncclCommAbort / ncclCommDestroy on such a
+// communicator join the blocked thread. So the init runs on a helper thread that owns its
+// result; the caller waits up to timeout_ms and otherwise returns VIP_ERR_COMM_TIMEOUT,
+// leaving the helper detached (the communicator is never handed out, the process keeps the
+// stuck thread until it exits).
+struct InitJob {
+    std::vector<ncclComm_t> comms;
+    std::atomic<int> status{0};
+    std::atomic<bool> done{false};
+    std::string error;
+};
+
+template <class F>
+int bounded_init(const std::shared_ptr<InitJob>& job, F&& body, int timeout_ms, std::vector<ncclComm_t>* out) {
+    std::thread([job, body]() mutable {
+        job->status = body(*job);
+        job->done = true;
+    }).detach();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!job->done.load()) {
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0);
+        if (ms.count() > timeout_ms) {
+            g_last_error = "communicator initialisation: not complete after " + std::to_string(timeout_ms) +
+                           " ms (a rank did not join)";
+            return VIP_ERR_COMM_TIMEOUT;
+        }
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    if (job->status != 0) {
+        g_last_error = job->error;
+        return job->status;
+    }
+    *out = job->comms;
+    return 0;
+}
 
 }  // namespace
 
@@ -224,11 +266,23 @@ int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, in
     if (!rc) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.blocking = 0;  // poll with a deadline instead of blocking for a missing rank
-        const ncclResult_t e = ncclCommInitRankConfig(&h->nccl, nranks, u, rank, &cfg);
-        if (e != ncclSuccess && e != ncclInProgress) rc = comm_fail(e, "ncclCommInitRankConfig");
-        if (!rc && h->nccl) rc = wait_comm(h->nccl, h->timeout_ms, "communicator initialisation");
+        const int dev = h->device;
+        auto job = std::make_shared<InitJob>();
+        std::vector<ncclComm_t> comms;
+        rc = bounded_init(
+            job,
+            [u, nranks, rank, dev](InitJob& j) {
+                j.comms.assign(1, nullptr);
+                if (hipSetDevice(dev) != hipSuccess) return (int)hipErrorInvalidDevice;
+                const ncclResult_t e = ncclCommInitRank(&j.comms[0], nranks, u, rank);
+                if (e != ncclSuccess) {
+                    j.error = std::string("ncclCommInitRank: ") + ncclGetErrorString(e);
+                    return (int)VIP_ERR_COMM;
+                }
+                return 0;
+            },
+            h->timeout_ms, &comms);
+        if (!rc) h->nccl = comms[0];
     }
     if (rc) {
         vip_shard_destroy(h);
@@ -254,19 +308,30 @@ int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* de
     if (!rc && transport == VIP_SHARD_RCCL) {
         // one communicator per device, initialised in one group (ncclCommInitAll's pattern)
         ncclUniqueId u;
-        ncclResult_t e = ncclGetUniqueId(&u);
-        if (e) rc = comm_fail(e, "ncclGetUniqueId");
-        if (!rc && (e = ncclGroupStart())) rc = comm_fail(e, "ncclGroupStart");
-        for (int i = 0; i < n && !rc; ++i) {
-            rc = (int)hipSetDevice(devices[i]);
-            ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-            cfg.blocking = 0;
-            if (!rc && (e = ncclCommInitRankConfig(&out[i]->nccl, n, u, i, &cfg)) && e != ncclInProgress)
-                rc = comm_fail(e, "ncclCommInitRankConfig");
-        }
-        e = ncclGroupEnd();
-        if (!rc && e != ncclSuccess && e != ncclInProgress) rc = comm_fail(e, "ncclGroupEnd (init)");
-        for (int i = 0; i < n && !rc; ++i) rc = wait_comm(out[i]->nccl, out[i]->timeout_ms, "communicator initialisation");
+        if (const ncclResult_t e = ncclGetUniqueId(&u)) rc = comm_fail(e, "ncclGetUniqueId");
+        std::vector<int> devs(devices, devices + n);
+        auto job = std::make_shared<InitJob>();
+        std::vector<ncclComm_t> comms;
+        if (!rc)
+            rc = bounded_init(
+                job,
+                [u, n, devs](InitJob& j) {
+                    j.comms.assign(n, nullptr);
+                    ncclResult_t e = ncclGroupStart();
+                    for (int i = 0; i < n && e == ncclSuccess; ++i) {
+                        if (hipSetDevice(devs[i]) != hipSuccess) return (int)hipErrorInvalidDevice;
+                        e = ncclCommInitRank(&j.comms[i], n, u, i);
+                    }
+                    const ncclResult_t e2 = ncclGroupEnd();
+                    if (e == ncclSuccess) e = e2;
+                    if (e != ncclSuccess) {
+                        j.error = std::string("ncclCommInitRank (group): ") + ncclGetErrorString(e);
+                        return (int)VIP_ERR_COMM;
+                    }
+                    return 0;
+                },
+                out[0]->timeout_ms, &comms);
+        for (int i = 0; i < n && !rc; ++i) out[i]->nccl = comms[i];
     }
     if (rc) {
         for (int i = 0; i < n; ++i) {
@@ -400,7 +465,7 @@ int vip_shard_destroy(vip_shard_t h) {
     if (!h) return 0;
     DeviceGuard guard;
     (void)hipSetDevice(h->device);
-    if (h->nccl) {
+    if (h->nccl) {  // only complete communicators are stored (bounded_init)
         ncclResult_t st = ncclSuccess;
         if (ncclCommGetAsyncError(h->nccl, &st) == ncclSuccess && st == ncclSuccess)
             (void)ncclCommDestroy(h->nccl);

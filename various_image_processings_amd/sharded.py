@@ -78,6 +78,17 @@ class SlabGeometry:
         return lo, hi
 
 
+def split_bands(geo: SlabGeometry) -> tuple[tuple[int, int], list[tuple[int, int]]]:
+    """Own rows split for overlapping the exchange (== vip_shard.hip interior/edges):
+    the interior (row0, rows) = (r, own - 2r) reads only own rows, so it can run while
+    the halos move; the two edge bands [(0, r), (own - r, r)] need the halos. Thin shards
+    (own <= 2r) have no interior and edge bands that tile the own rows."""
+    r, own = geo.radius, geo.own
+    top = min(r, own)
+    b0 = max(own - r, top)
+    return (r, max(0, own - 2 * r)), [(0, top), (b0, own - b0)]
+
+
 def exchange_halo(slab, geo: SlabGeometry, group=None) -> None:
     """Fill slab's halo rows from the neighbouring ranks (blocking).
 
@@ -162,12 +173,30 @@ class ShardedBilateral:
         self.impl = cls(width, self.geo.slab_rows, ksize, sigma_space, sigma_color, numerics)
         self.adaptive = adaptive
 
-    def filter(self, slab, out, stream=None, exchange: bool = True) -> None:
-        """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3)."""
+    def filter(self, slab, out, stream=None, exchange: bool = True, split: bool = True) -> None:
+        """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3).
+        exchange and split: the interior rows first (they read no halo), then the halo
+        exchange, then the two edge bands (split_bands) -- the kernel's work that can
+        proceed while the halos move is queued ahead of the exchange."""
+        g = self.geo
+        (i0, ni), edges = split_bands(g)
+        if exchange and split and g.world > 1 and ni > 0:
+            self._rows(slab, out, i0, ni, stream)
+            _exchange_on(slab, g, stream)
+            for e0, ne in edges:
+                self._rows(slab, out, e0, ne, stream)
+            return
         if exchange:
-            _exchange_on(slab, self.geo, stream)
+            _exchange_on(slab, g, stream)
+        self._rows(slab, out, 0, g.own, stream)
+
+    def _rows(self, slab, out, row0: int, rows: int, stream) -> None:
+        """Own rows [row0, row0 + rows) of the slab -> the same rows of out."""
+        if rows <= 0:
+            return
         lo, hi = self.geo.clamp_range()
-        self.impl.run_rows(slab, out, self.geo.own, self.geo.radius, lo, hi, stream=stream)
+        o = out + row0 * self.geo.width * 3 if isinstance(out, int) else out[row0:row0 + rows]
+        self.impl.run_rows(slab, o, rows, self.geo.radius + row0, lo, hi, stream=stream)
 
 
 def texture_halo_rows(ksize: int) -> int:
