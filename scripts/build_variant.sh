@@ -15,5 +15,5 @@ hipcc $F -DVIP_ONLY_R7 -c vip_adaptive.hip -o /tmp/var_$name/am.o
 # the texture, C ABI and C++ API objects of the in-place CMake build (__graft_entry__.build())
 O=../../build/cmake/CMakeFiles
 hipcc --offload-arch=gfx950 -shared -o ../../variants/$name.so /tmp/var_$name/*.o \
-  $(ls $O/vip_{texture,capi}.dir/various_image_processings_amd/csrc/*.o $O/vip_hip.dir/various_image_processings_amd/csrc/*.o)
+  $(ls $O/vip_{texture,capi,stencil_rt}.dir/various_image_processings_amd/csrc/*.o $O/vip_hip.dir/various_image_processings_amd/csrc/*.o)
 echo built variants/$name.so

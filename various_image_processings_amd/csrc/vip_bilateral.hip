@@ -67,8 +67,15 @@ struct FoldRank {  // table index of tap (|ky|, |kx|)
             for (int x = 0; x <= R; ++x) t[y * (R + 1) + x] = disc_r2_rank(R, x * x + y * y);
     }
 };
+// VIP_BIL_MIN_WPE (build knob, experiments): at least this many waves per SIMD, i.e. a
+// VGPR cap of 512 / N, so that a smaller workgroup leaves registers for a second kernel
+#ifdef VIP_BIL_MIN_WPE
+#define VIP_BIL_WPE_ATTR __attribute__((amdgpu_waves_per_eu(VIP_BIL_MIN_WPE)))
+#else
+#define VIP_BIL_WPE_ATTR
+#endif
 template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false>
-__global__ __launch_bounds__(WAVES * 64) void bilateral_kernel(const StencilArgs a) {
+__global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
     constexpr int TH = WAVES * 4;
