@@ -126,6 +126,14 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
  * 16, 8 or 4 forces one. Results are identical for every setting (only the tiling
  * changes). The environment variable VIP_BIL_WAVES sets the initial value. */
 int vip_bilateral_set_waves(int waves);
+/* Companion knob: the tile shape of the same kernel for radius <= 8. 0 (default) = chosen
+ * per launch with the wave count (small frames and the slabs of a frame split over many
+ * GPUs take 256-pixel tiles, one row per wave and 4 outputs per thread: half the serial
+ * work per thread); 1 forces 128-pixel tiles (4 rows per wave, 8 outputs per thread),
+ * 2 forces 256-pixel tiles. Results are identical for every setting. The environment
+ * variable VIP_BIL_WIDE sets the initial value. A forced wave count with mode 0 keeps
+ * 128-pixel tiles. */
+int vip_bilateral_set_wide(int mode);
 
 /* ---- adaptive bilateral: CudaAdaptiveBilateralFilter
  *      (include/cuda/adaptive_bilateral_filter.hpp:9-19, src/adaptive_bilateral_filter_impl.cu:117-191) ---- */

@@ -1,6 +1,6 @@
-"""Bilateral launch time per frame size for each wave count of the plain kernel
-(VIP_BIL_WAVES=16|8|4, or the library's own choice), one subprocess per setting (the
-knob is read once per process). Every forced setting's output must equal the
+"""Bilateral launch time per frame size for each tiling of the plain kernel
+(VIP_BIL_WAVES=16|8|4 x VIP_BIL_WIDE=1 (128-px tiles) | 2 (256-px tiles), or the
+library's own choice), one subprocess per setting (the knobs are read once per process). Every forced setting's output must equal the
 auto setting's byte for byte (same arithmetic, different tiles).
 usage: python scripts/small_frame_bench.py [out.json]"""
 import json
@@ -14,7 +14,10 @@ sys.path.insert(0, ".")
 from various_image_processings_amd.filters import _BilateralImpl
 torch.cuda.set_device(0)
 cases = [("c1_lenna_r5", 512, 512, 11), ("720p_r7", 1280, 720, 15), ("1080p_r7", 1920, 1080, 15),
-         ("4k_r7", 3840, 2160, 15), ("720p_r3", 1280, 720, 7)]
+         ("4k_r7", 3840, 2160, 15), ("720p_r3", 1280, 720, 7),
+         # slabs of the 4K frame at 2 / 4 / 8 GPUs and a 7-row edge band (strong scaling)
+         ("4k_slab1080_r7", 3840, 1080, 15), ("4k_slab540_r7", 3840, 540, 15), ("4k_slab270_r7", 3840, 270, 15),
+         ("4k_band7_r7", 3840, 7, 15)]
 res, sums = {}, {}
 g = torch.Generator(device="cuda"); g.manual_seed(7)
 for name, W, H, k in cases:
@@ -36,11 +39,13 @@ for name, W, H, k in cases:
 print(json.dumps({"us": res, "sums": sums}))
 '''
 out = {}
-for w in ["auto", "16", "8", "4"]:
+for w in ["auto", "16", "8", "4", "16w", "8w", "4w"]:
     env = dict(os.environ)
     env.pop("VIP_BIL_WAVES", None)
+    env.pop("VIP_BIL_WIDE", None)
     if w != "auto":
-        env["VIP_BIL_WAVES"] = w
+        env["VIP_BIL_WAVES"] = w.rstrip("w")
+        env["VIP_BIL_WIDE"] = "2" if w.endswith("w") else "1"
     r = subprocess.run([sys.executable, "-c", CODE], capture_output=True, text=True, timeout=240, env=env)
     if r.returncode != 0:
         print(w, r.stderr[-800:], flush=True)

@@ -92,8 +92,13 @@ def test_bilateral_wave_knob_validates():
             assert L.vip_bilateral_set_waves(w) == 0
         for w in (12, 2, -1, 32):
             assert L.vip_bilateral_set_waves(w) == 10001
+        for m in (0, 1, 2):
+            assert L.vip_bilateral_set_wide(m) == 0
+        for m in (3, -1):
+            assert L.vip_bilateral_set_wide(m) == 10001
     finally:
         L.vip_bilateral_set_waves(0)
+        L.vip_bilateral_set_wide(0)
 
 
 def test_reference_api_surface():

@@ -66,15 +66,32 @@ def test_bilateral_large_frame(dev, oracle, k, ss, sc):
 # (vip_bilateral_set_waves, radius <= 8). Every forced wave count must give the oracle's
 # bytes; 1300x400 has 275 tiles at 4 waves, so some workgroups take two.
 @pytest.mark.parametrize("waves", [16, 8, 4])
+@pytest.mark.parametrize("wide", [1, 2])
 @pytest.mark.parametrize("k", [3, 11, 17])
-def test_bilateral_forced_waves(dev, oracle, waves, k):
+def test_bilateral_forced_waves(dev, oracle, waves, wide, k):
+    """wide = 2: 256-pixel tiles, one row per wave, 4 outputs per thread (vip_bilateral_set_wide)."""
     img = oracle.random_image(1300, 400)
     vip.set_bilateral_waves(waves)
+    vip.set_bilateral_wide(wide)
     try:
         got = _bilateral_gpu(dev, img, k)
     finally:
         vip.set_bilateral_waves(0)
+        vip.set_bilateral_wide(0)
     want = oracle.bilateral(img, k, threads=16)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (7, 3840), (270, 3840), (17, 300), (512, 512), (33, 257)])
+@pytest.mark.parametrize("k", [5, 15])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_bilateral_wide_tiles_auto(dev, oracle, shape, k, numerics, profile):
+    """Frames the per-launch choice gives 256-pixel tiles (a 7-row edge band, the 270-row
+    slab of the 4K frame at 8 GPUs, lenna 512^2), ragged widths, both profiles."""
+    h, w = shape
+    img = oracle.random_u8(h * w * 3).reshape(h, w, 3)
+    got = _bilateral_gpu(dev, img, k, numerics=numerics)
+    want = oracle.bilateral(img, k, profile=profile, threads=16)
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
@@ -82,6 +99,9 @@ def test_bilateral_set_waves_rejects_other_counts():
     with pytest.raises(vip.VipError):
         vip.set_bilateral_waves(12)
     vip.set_bilateral_waves(0)
+    with pytest.raises(vip.VipError):
+        vip.set_bilateral_wide(3)
+    vip.set_bilateral_wide(0)
 
 
 @pytest.mark.parametrize("k", [3, 9, 15, 25, 31])

@@ -27,6 +27,7 @@ from .filters import (  # noqa: F401
     device_synchronize,
     max_ksize,
     set_bilateral_waves,
+    set_bilateral_wide,
     set_stencil_path,
 )
 

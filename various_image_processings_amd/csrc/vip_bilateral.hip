@@ -74,11 +74,11 @@ struct FoldRank {  // table index of tap (|ky|, |kx|)
 #else
 #define VIP_BIL_WPE_ATTR
 #endif
-template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false>
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false, int TPR = 16>
 __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(const StencilArgs a) {
-    using G = Geom<R, P>;
+    using G = Geom<R, P, TPR>;
     constexpr int NT = WAVES * 64;
-    constexpr int TH = WAVES * 4;
+    constexpr int TH = WAVES * G::RPW;
     constexpr bool ROW_UNROLL = R <= VIP_BIL_UNROLL_MAX_R;  // straight-line rows (for_each_row)
     constexpr int ROWS = TH + 2 * R;
     constexpr int PLANE = ROWS * G::S;
@@ -92,15 +92,15 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int tx = lane & 15;
-    const int ty = wave * 4 + (lane >> 4);
+    const int tx = lane % TPR;
+    const int ty = wave * G::RPW + lane / TPR;
     const uint32_t lane4 = (uint32_t)(lane & (COPIES - 1)) << 2;  // this lane's LUT copy
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     VIP_RT_STAMP(0);
     // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
     int tile = blockIdx.x;
-    TilePrefetch<R, ROWS, NT, P> pg, ps;
+    TilePrefetch<R, ROWS, NT, P, TPR> pg, ps;
     LutStage<NT, NTAB * NE, COPIES> ls;  // once per workgroup; its reads go out first
     ls.load(FOLD ? a.fold : a.color);
     {
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
             pg.issue(a.guide, a.guide_pitch, a, nx0, ny0);
             if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
         }
-        if (ty0 + wave * 4 < a.out_rows) {  // wave-uniform: skip rows past the frame
+        if (ty0 + wave * G::RPW < a.out_rows) {  // wave-uniform: skip rows past the frame
             uint32_t ctr[P];  // centre pixels of the guide (== src for the plain filter)
             {
                 const uint4* c = reinterpret_cast<const uint4*>(gplane + (ty + R) * G::S + tx * P + G::L);
@@ -225,31 +225,52 @@ constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : (R > 8 ? VIP_BIL
 #endif
 
 // Small frames (plain filter, R <= VIP_BIL_SMALL_MAX_R): a frame with fewer 128 x 64
-// tiles than CUs leaves CUs idle (C1's 512 x 512 lenna: 32 tiles on 256 CUs). The
-// same kernel on 8 or 4 waves has 128 x 32 / 128 x 16 tiles, so more CUs work, each
-// with fewer waves per SIMD. Chosen per launch by a per-CU time model:
-// rounds(W) * W * cost(W), cost = the per-wave slowdown at W/4 waves per SIMD
-// (measured); vip_bilateral_set_waves / VIP_BIL_WAVES=16|8|4 force one.
+// tiles than CUs leaves CUs idle (C1's 512 x 512 lenna: 32 tiles on 256 CUs; a 270-row
+// slab of the 4K frame at 8 GPUs: 150). Two ways to spread it: fewer waves per workgroup
+// (8 or 4: 128 x 32 / 128 x 16 tiles, more CUs busy, fewer waves per SIMD), and the
+// "wide" tiling -- one 256-pixel row per wave, 4 outputs per thread -- which halves the
+// serial tap work of a thread, so a launch whose tiles fit in one round ends sooner
+// (every thread of a 16-wave tile runs its 8 outputs x 149 taps back to back: ~47 us
+// at r = 7, whatever the frame size). Chosen per launch by a per-CU time model,
+// rounds * waves * cost(waves) * work(P): cost = 1, 1.25, 1.8 at 4, 2, 1 waves per SIMD,
+// work = 1 for 8 outputs per thread, kWideWork for 4 (half the taps plus the extra byte
+// conversions and apron rows). vip_bilateral_set_waves / VIP_BIL_WAVES and
+// vip_bilateral_set_wide / VIP_BIL_WIDE force either.
 #ifndef VIP_BIL_SMALL_MAX_R
 #define VIP_BIL_SMALL_MAX_R 8
 #endif
-inline int small_frame_waves(int tiles_x, int out_rows) {
+#ifndef VIP_BIL_WIDE_WORK
+#define VIP_BIL_WIDE_WORK 0.55f
+#endif
+struct Tiling {
+    int waves;
+    bool wide;
+};
+inline Tiling small_frame_tiling(int width, int out_rows) {
     const int forced = bilateral_forced_waves();
-    if (forced) return forced;
+    const int fwide = bilateral_forced_wide();  // 0 auto, 1 narrow, 2 wide
     const int cus = device_cus();
     const int cand[3] = {16, 8, 4};
     const float cost[3] = {1.0f, 1.25f, 1.8f};
-    int best = 16;
+    Tiling best{16, false};
     float best_t = 0.f;
-    for (int i = 0; i < 3; ++i) {
-        const long long tiles = (long long)tiles_x * ((out_rows + cand[i] * 4 - 1) / (cand[i] * 4));
-        const float t = (float)((tiles + cus - 1) / cus) * cand[i] * cost[i];
-        if (i == 0 || t < best_t) best = cand[i], best_t = t;
+    bool first = true;
+    for (int wide = 0; wide < 2; ++wide) {
+        if ((fwide == 1 && wide) || (fwide == 2 && !wide) || (fwide == 0 && forced && wide)) continue;
+        const int tw = wide ? 256 : 128, rpw = wide ? 1 : 4;
+        const long long tiles_x = (width + tw - 1) / tw;
+        for (int i = 0; i < 3; ++i) {
+            if (forced && cand[i] != forced) continue;
+            const int th = cand[i] * rpw;
+            const long long tiles = tiles_x * ((out_rows + th - 1) / th);
+            const float t = (float)((tiles + cus - 1) / cus) * cand[i] * cost[i] * (wide ? VIP_BIL_WIDE_WORK : 1.f);
+            if (first || t < best_t) best = Tiling{cand[i], wide != 0}, best_t = t, first = false;
+        }
     }
     return best;
 }
 
-template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES>
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE = false>
 static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream);
 
 template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false>
@@ -261,26 +282,34 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
-        const int w = small_frame_waves((a.width + Geom<R, P>::TW - 1) / Geom<R, P>::TW, a.out_rows);
-        if (w == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8>(a, stream);
-        if (w == 4) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4>(a, stream);
+        const Tiling t = small_frame_tiling(a.width, a.out_rows);
+        if (t.wide) {
+            if (t.waves == 16) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
+            if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8, true>(a, stream);
+            return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4, true>(a, stream);
+        }
+        if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8>(a, stream);
+        if (t.waves == 4) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4>(a, stream);
     }
     return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, WAVES>(a, stream);
 }
 
-template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES>
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE>
 static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
-    constexpr int P = outputs_per_thread<R, PLANES>();
+    constexpr int P = WIDE ? 4 : outputs_per_thread<R, PLANES>();
+    constexpr int TPR = WIDE ? 64 : 16;  // threads per tile row
+    using G = Geom<R, P, TPR>;
     constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
-    constexpr int TH = WAVES * 4;
-    constexpr int LDS = lds_bytes<R, WAVES, PLANES, LUTW, P>();
-    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD>;
+    constexpr int TH = WAVES * G::RPW;
+    constexpr int LDS = lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
+    static_assert(LDS <= kLdsBudget, "tile does not fit LDS");
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
-    args.tiles_x = (a.width + Geom<R, P>::TW - 1) / Geom<R, P>::TW;
+    args.tiles_x = (a.width + G::TW - 1) / G::TW;
     args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total);

@@ -164,6 +164,12 @@ static std::atomic<int> g_bil_waves{[] {
     return valid_waves(w) ? w : 0;
 }()};
 int bilateral_forced_waves() { return g_bil_waves.load(std::memory_order_relaxed); }
+static std::atomic<int> g_bil_wide{[] {
+    const char* e = getenv("VIP_BIL_WIDE");
+    const int w = e ? atoi(e) : 0;
+    return w >= 0 && w <= 2 ? w : 0;
+}()};
+int bilateral_forced_wide() { return g_bil_wide.load(std::memory_order_relaxed); }
 
 }  // namespace vip
 
@@ -248,6 +254,12 @@ int vip_set_stencil_path(int path) {
 int vip_bilateral_set_waves(int waves) {
     if (!valid_waves(waves)) return VIP_ERR_INVALID_ARGUMENT;
     g_bil_waves.store(waves, std::memory_order_relaxed);
+    return 0;
+}
+
+int vip_bilateral_set_wide(int mode) {
+    if (mode < 0 || mode > 2) return VIP_ERR_INVALID_ARGUMENT;
+    g_bil_wide.store(mode, std::memory_order_relaxed);
     return 0;
 }
 

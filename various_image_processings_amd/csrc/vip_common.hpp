@@ -80,4 +80,7 @@ inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned 
 
 // vip_bilateral_set_waves (vip_capi.hip): 0 = per-launch choice, else 16 / 8 / 4.
 int bilateral_forced_waves();
+// vip_bilateral_set_wide: 0 = per-launch choice, 1 = 128-pixel tiles (8 outputs per
+// thread), 2 = 256-pixel tiles (4 outputs per thread, one row per wave).
+int bilateral_forced_wide();
 }  // namespace vip

@@ -105,35 +105,42 @@ __device__ __forceinline__ int xcd_tile(int slot, int total) {
     return base + (b & 7) * (grid >> 3) + (b >> 3);
 }
 
-// P outputs per thread (8, or 4 for register-heavy kernels), 16 threads per tile row.
+// P outputs per thread (8, or 4 for register-heavy kernels), TPR threads per tile row:
+// 16 (a wave covers 4 tile rows, the default) or 64 ("wide": one 256-pixel row per wave,
+// P = 4 -- half the serial work per thread, for frames too small to fill the chip).
 // S makes the ds_read_b128 row loads conflict-free: with P = 8 the 16 lanes of a
-// b128 group read words tx*8 + 4c of rows ty, ty+1 -> S = 4 (mod 8); with P = 4
-// they read 64 contiguous words per row -> S = 0 (mod 64).
-template <int R, int P = kP>
+// b128 group read words tx*8 + 4c of rows ty, ty+1 -> S = 4 (mod 8); with P = 4 and
+// 16 threads per row they read 64 contiguous words per row -> S = 0 (mod 64); with 64
+// threads per row a wave reads 256 contiguous words of ONE row, whose lane groups
+// ({0-3, 12-15, 20-27} ...) always cover 64 distinct banks -> any S.
+template <int R, int P = kP, int TPR = 16>
 struct Geom {
-    static_assert(P == 8 || P == 4, "P");
-    static constexpr int TW = 16 * P;                        // tile width in pixels
+    static_assert((P == 8 && TPR == 16) || (P == 4 && (TPR == 16 || TPR == 64)), "P, TPR");
+    static constexpr int TW = TPR * P;                       // tile width in pixels
+    static constexpr int RPW = 64 / TPR;                     // tile rows per wave
     static constexpr int L = round_up(R, 4);                 // left/right apron, 4-px aligned
-    static constexpr int S = P == 8 ? round_up(TW + 2 * L, 8) + 4 : round_up(TW + 2 * L, 64);
+    static constexpr int S = P == 8 ? round_up(TW + 2 * L, 8) + 4
+                                    : (TPR == 64 ? round_up(TW + 2 * L, 4) : round_up(TW + 2 * L, 64));
     static constexpr int GROUPS = (TW + 2 * L) / 4;          // 4-pixel groups per tile row
 };
 
 // Largest wave count (<= MAXW: 16, 12, 8 or 4) whose LUT (LUTW words) + plane(s) fit
 // the CU's LDS.
-template <int R, int PLANES, int MAXW = 16, int LUTW = lut_words(false), int P = kP>
+template <int R, int PLANES, int MAXW = 16, int LUTW = lut_words(false), int P = kP, int TPR = 16>
 constexpr int pick_waves() {
     constexpr int cand[4] = {16, 12, 8, 4};
     for (int w : cand) {
         if (w > MAXW) continue;
-        const long long bytes = 4LL * LUTW + 4LL * PLANES * (w * 4 + 2 * R) * Geom<R, P>::S;
+        const long long bytes =
+            4LL * LUTW + 4LL * PLANES * (w * Geom<R, P, TPR>::RPW + 2 * R) * Geom<R, P, TPR>::S;
         if (bytes <= kLdsBudget) return w;
     }
     return 0;
 }
 
-template <int R, int WAVES, int PLANES, int LUTW = lut_words(false), int P = kP>
+template <int R, int WAVES, int PLANES, int LUTW = lut_words(false), int P = kP, int TPR = 16>
 constexpr int lds_bytes() {
-    return 4 * LUTW + 4 * PLANES * (WAVES * 4 + 2 * R) * Geom<R, P>::S;
+    return 4 * LUTW + 4 * PLANES * (WAVES * Geom<R, P, TPR>::RPW + 2 * R) * Geom<R, P, TPR>::S;
 }
 
 // Calls f(std::integral_constant<int, HW>) for the runtime circle half-width hw.
@@ -224,9 +231,9 @@ __device__ __forceinline__ float div_exact(uint32_t s, float d, float rd) {
 // byte loads otherwise) and returns at once; commit() unpacks RGB to RGBX words
 // and writes the LDS plane. A persistent workgroup issues tile t+1 before it
 // computes tile t, so HBM latency hides under the VALU-bound tap loop.
-template <int R, int ROWS, int NT, int P = kP>
+template <int R, int ROWS, int NT, int P = kP, int TPR = 16>
 struct TilePrefetch {
-    using G = Geom<R, P>;
+    using G = Geom<R, P, TPR>;
     static constexpr int NG = ROWS * G::GROUPS;
     static constexpr int K = (NG + NT - 1) / NT;
     uint32_t raw[K][3];

@@ -29,7 +29,7 @@ from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
 __all__ = [
     "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
     "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
-    "set_bilateral_waves", "set_stencil_path", "max_ksize",
+    "set_bilateral_waves", "set_bilateral_wide", "set_stencil_path", "max_ksize",
 ]
 
 
@@ -90,6 +90,13 @@ def max_ksize(filter_kind: int) -> int:
     """Largest ksize a filter accepts (include/vip.h vip_max_ksize): what the reference
     runs -- bilateral 65, joint 47, adaptive 63, texture 24."""
     return int(lib().vip_max_ksize(int(filter_kind)))
+
+
+def set_bilateral_wide(mode: int = 0) -> None:
+    """Companion tuning knob (include/vip.h vip_bilateral_set_wide): 0 = tile shape chosen
+    per launch, 1 = 128-pixel tiles (8 outputs per thread), 2 = 256-pixel tiles (one row
+    per wave, 4 outputs per thread). Outputs are identical for every setting."""
+    call("vip_bilateral_set_wide", int(mode))
 
 
 def set_bilateral_waves(waves: int = 0) -> None:
