@@ -549,6 +549,31 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             step(i_settle)
             i_settle += 1
         torch.cuda.synchronize(dev)
+    if native:
+        # vip_shard_set_split: interior rows under the exchange then the two edge bands,
+        # or one launch after the exchange (fewer launches; with two frames in flight the
+        # exchange still overlaps the other frame's kernel). Which is faster depends on the
+        # exchange's latency on this machine: time both (max over ranks) and keep the faster.
+        trial = {}
+        n_trial = 40
+        for sp in (True, False):
+            sb.set_split(sp)
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(n_trial):
+                step(i_settle)
+                i_settle += 1
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            trial[sp] = float(dt[0])
+        best = min(trial, key=trial.get)
+        sb.set_split(best)
+        res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best
+                            else "one launch after the exchange",
+                            trial_ms_per_step={"split": round(trial[True], 4), "one_launch": round(trial[False], 4)})
     res["settle_steps"] = i_settle
     base = i_settle
     for i in range(args.warmup):
@@ -751,6 +776,7 @@ def main():
         **({"frame_ms_in_flight": round(m["frame_ms"], 4)} if world == 1 and S > 1 else {}),
         "settle": {"seconds": args.settle_s, "steps": m["settle_steps"]},
         **{k_: round(v, 4) for k_, v in parts.items()},
+        **({"split": m["split"]} if m.get("split") else {}),
         **({"weak": weak} if weak else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -21,7 +21,10 @@
  *
  * Overlap: a run enqueues the exchange on the shard's own communication stream and, at
  * the same time, the interior rows [r, own - r) (which read only own rows) on the
- * caller's stream; the two r-row edge bands follow once the halos have arrived.
+ * caller's stream; the two r-row edge bands follow once the halos have arrived
+ * (vip_shard_set_split(h, 1), the default). With split 0 the run filters all own rows in
+ * one launch after the exchange: fewer launches, and with frames in flight on two streams
+ * the exchange of one frame still overlaps the other frame's kernel.
  *
  * Transports: RCCL (one communicator per rank; ncclSend/ncclRecv between row neighbours
  * in one group, no collective) or LOCAL (all slabs in one process on one device, halos by
@@ -29,9 +32,10 @@
  * single GPU).
  *
  * Return value: 0, a hipError_t, a VIP_ERR_* code (vip.h) or VIP_ERR_COMM /
- * VIP_ERR_COMM_TIMEOUT below. Communicator creation never blocks past its timeout: it
- * runs RCCL's non-blocking initialisation, polls it until the deadline, then aborts the
- * communicator and returns VIP_ERR_COMM_TIMEOUT.
+ * VIP_ERR_COMM_TIMEOUT below. Communicator creation never blocks past its timeout: RCCL's
+ * initialisation runs on a helper thread, and at the deadline the call returns
+ * VIP_ERR_COMM_TIMEOUT, leaving the helper detached (RCCL blocks in its bootstrap while a
+ * rank is missing, and aborting such a communicator joins the blocked thread).
  */
 #ifndef VIP_SHARD_H
 #define VIP_SHARD_H
@@ -76,6 +80,11 @@ int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, in
 int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* devices, int kind, int width,
                            int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
                            int timeout_ms);
+
+/* 1 (default): interior rows during the exchange, then the two edge bands; 0: one launch
+ * over the own rows after the exchange. Same bytes either way. For groups, set it on
+ * every member. */
+int vip_shard_set_split(vip_shard_t h, int split);
 
 /* Geometry of a shard: its first frame row, own rows and halo rows (r). */
 int vip_shard_geometry(vip_shard_t h, int* row_begin, int* own_rows, int* halo_rows);

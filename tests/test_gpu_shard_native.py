@@ -33,10 +33,11 @@ def _single(dev, img, k, adaptive):
     return dev.get(d)
 
 
-def _run_group(dev, img, k, n, adaptive, transport=S.VIP_SHARD_LOCAL, devices=None):
+def _run_group(dev, img, k, n, adaptive, transport=S.VIP_SHARD_LOCAL, devices=None, split=True):
     torch = dev.torch_
     h, w, _ = img.shape
     g = ShardGroup(n, w, h, k, transport=transport, devices=devices, adaptive=adaptive)
+    g.set_split(split)
     slabs, outs, streams = [], [], []
     for geo in g.geos:
         b, e = geo.rows
@@ -57,8 +58,9 @@ def _run_group(dev, img, k, n, adaptive, transport=S.VIP_SHARD_LOCAL, devices=No
 def test_local_group_equals_single_launch_4k(dev, oracle, n, adaptive):
     img = oracle.random_image(3840, 2160)
     want = _single(dev, img, 15, adaptive)
-    got = _run_group(dev, img, 15, n, adaptive)
-    assert np.array_equal(got, want)
+    for split in (True, False):
+        got = _run_group(dev, img, 15, n, adaptive, split=split)
+        assert np.array_equal(got, want), split
 
 
 @pytest.mark.parametrize("shape,k,n", [((530, 700), 31, 8), ((77, 300), 9, 5), ((40, 131), 15, 5), ((64, 129), 65, 2)])
@@ -104,12 +106,14 @@ def test_rccl_single_rank_native_shard_timed(dev, oracle):
     s.filter(slab, out)
     want = _single(dev, img, 15, False)
     assert np.array_equal(dev.get(out), want)
-    out.zero_()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    s.filter_timed(slab, out, ev)
-    torch.cuda.synchronize()
-    assert np.array_equal(dev.get(out), want)
-    assert ev[0].elapsed_time(ev[3]) > 0
+    for split in (True, False):
+        s.set_split(split)
+        out.zero_()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        s.filter_timed(slab, out, ev)
+        torch.cuda.synchronize()
+        assert np.array_equal(dev.get(out), want)
+        assert ev[0].elapsed_time(ev[3]) > 0
 
 
 def test_rccl_missing_peer_times_out():

@@ -109,6 +109,7 @@ struct vip_shard_s {
     hipEvent_t ev_in = nullptr;  // own rows written (on the caller's stream)
     hipEvent_t ev_x = nullptr;   // halos received (on comm)
     ncclComm_t nccl = nullptr;   // VIP_SHARD_RCCL
+    int split = 1;               // interior rows under the exchange, then the edge bands
     bool above() const { return rank > 0 && r > 0; }
     bool below() const { return rank < nranks - 1 && r > 0; }
     int slab_rows() const { return own + 2 * r; }
@@ -342,6 +343,12 @@ int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* de
     return rc;
 }
 
+int vip_shard_set_split(vip_shard_t h, int split) {
+    if (!h || (split != 0 && split != 1)) return VIP_ERR_INVALID_ARGUMENT;
+    h->split = split;
+    return 0;
+}
+
 int vip_shard_geometry(vip_shard_t h, int* row_begin, int* own_rows, int* halo_rows) {
     if (!h || !row_begin || !own_rows || !halo_rows) return VIP_ERR_INVALID_ARGUMENT;
     *row_begin = h->row_begin;
@@ -377,6 +384,13 @@ static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
     }
     if (!rc) rc = mark(events, 1, h->comm);
     if (!rc) rc = (int)hipEventRecord(h->ev_x, h->comm);
+    if (!h->split) {  // one launch over the own rows once the halos are in
+        if (!rc) rc = mark(events, 2, s);
+        if (!rc) rc = (int)hipStreamWaitEvent(s, h->ev_x, 0);
+        if (!rc) rc = filter_rows(h, slab, out, out_pitch, 0, h->own, s);
+        if (!rc) rc = mark(events, 3, s);
+        return rc;
+    }
     if (!rc) rc = interior(h, slab, out, out_pitch, s);
     if (!rc) rc = mark(events, 2, s);
     if (!rc) rc = (int)hipStreamWaitEvent(s, h->ev_x, 0);
@@ -448,8 +462,14 @@ int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* 
         }
         for (int i = 0; i < n; ++i) {
             VIP_HIP_TRY(hipSetDevice(hs[i]->device));
+            const hipEvent_t x = rccl ? hs[i]->ev_x : hs[0]->ev_x;
+            if (!hs[i]->split) {
+                VIP_HIP_TRY(hipStreamWaitEvent(st(i), x, 0));
+                if (const int rc = filter_rows(hs[i], slabs[i], outs[i], out_pitch, 0, hs[i]->own, st(i))) return rc;
+                continue;
+            }
             if (const int rc = interior(hs[i], slabs[i], outs[i], out_pitch, st(i))) return rc;
-            VIP_HIP_TRY(hipStreamWaitEvent(st(i), rccl ? hs[i]->ev_x : hs[0]->ev_x, 0));
+            VIP_HIP_TRY(hipStreamWaitEvent(st(i), x, 0));
             if (const int rc = edges(hs[i], slabs[i], outs[i], out_pitch, st(i))) return rc;
         }
         return 0;

@@ -293,6 +293,12 @@ class NativeShard:
                sigma_space, sigma_color, numerics, world, rank, idb, int(timeout_ms))
         self.geo = SlabGeometry(width, frame_height, ksize // 2, rank, world)
 
+    def set_split(self, split: bool) -> None:
+        """vip_shard_set_split: interior rows during the exchange, then the edge bands
+        (True, default), or one launch after the exchange (False)."""
+        from . import _shard_lib as S
+        S.call("vip_shard_set_split", self._h, 1 if split else 0)
+
     def filter(self, slab, out, stream=None) -> None:
         """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3). Asynchronous."""
         from . import _shard_lib as S
@@ -340,6 +346,11 @@ class ShardGroup:
         S.call("vip_shard_create_group", self._hs, n, transport, devs, _shard_kind(adaptive), width, frame_height,
                ksize, sigma_space, sigma_color, numerics, int(timeout_ms))
         self.geos = [SlabGeometry(width, frame_height, ksize // 2, i, n) for i in range(n)]
+
+    def set_split(self, split: bool) -> None:
+        from . import _shard_lib as S
+        for i in range(self.n):
+            S.call("vip_shard_set_split", self._hs[i], 1 if split else 0)
 
     def filter(self, slabs, outs, streams) -> None:
         import ctypes
