@@ -114,6 +114,12 @@ def lenna_png(tmp_path_factory, lenna):
     ("adaptive", ["15", "10", "30"]),
     ("texture", []),                    # defaults: ksize 9, nitr 3
     ("texture", ["5", "5"]),            # C4's parameters
+    # the largest ksizes the reference runs, and ksize 1, through the C++ classes
+    ("bilateral", ["65", "10", "30"]),
+    ("bilateral", ["1", "10", "30"]),
+    ("joint", ["47", "10", "30"]),
+    ("adaptive", ["63", "10", "30"]),
+    ("texture", ["24", "1"]),
 ])
 def test_vip_filter_image_files(lenna_png, lenna, oracle, mode, params):
     exe = os.path.join(ROOT, "samples", "vip_filter")
