@@ -1,6 +1,7 @@
 """Per-rank compute of C2 strong scaling on one GPU: a (3840 x (2160/N + 14)) slab of the
-4K frame filtered (a) as one launch over its own rows, (b) split like vip_shard_run --
-interior rows, then the two 7-row edge bands -- with 1 and 2 frames in flight.
+4K frame filtered (a) as one launch over its own rows, (b) split -- interior rows, then
+the two 7-row edge bands on the same stream, (c) split like vip_shard_run -- the edge
+bands on a side stream concurrent with the interior -- with 1 and 2 frames in flight.
 Excludes the exchange. Prints one JSON line per N."""
 import json
 import sys
@@ -23,19 +24,27 @@ for n in (1, 2, 4, 8):
     outs = [torch.empty((own, W, 3), dtype=torch.uint8, device="cuda") for _ in range(4)]
     (i0, ni), edges = split_bands(geo)
     res = {"n": n, "own_rows": own}
-    for mode in ("full", "split"):
+    for mode in ("full", "split", "split_side"):
         for S in (1, 2):
             streams = [torch.cuda.Stream() for _ in range(S)]
+            sides = [torch.cuda.Stream() for _ in range(S)]  # vip_shard's communication streams
 
             def frame(i):
                 s = streams[i % S]
                 sl, o = slabs[i % 4], outs[i % 4]
                 if mode == "full":
                     impl.run_rows(sl, o, own, r, lo, hi, stream=s)
-                else:
+                elif mode == "split":  # edges after the interior, one stream
                     impl.run_rows(sl, o[i0:i0 + ni], ni, r + i0, lo, hi, stream=s)
                     for e0, ne in edges:
                         impl.run_rows(sl, o[e0:e0 + ne], ne, r + e0, lo, hi, stream=s)
+                else:  # vip_shard_run: edges on the side stream, concurrent with the interior
+                    c = sides[i % S]
+                    c.wait_stream(s)
+                    for e0, ne in edges:
+                        impl.run_rows(sl, o[e0:e0 + ne], ne, r + e0, lo, hi, stream=c)
+                    impl.run_rows(sl, o[i0:i0 + ni], ni, r + i0, lo, hi, stream=s)
+                    s.wait_stream(c)
             t0 = time.perf_counter()
             i = 0
             while time.perf_counter() - t0 < 0.7:
