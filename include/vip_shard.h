@@ -19,10 +19,10 @@
  * reference's replicate border (reads clamp to the own rows), so the sharded result is
  * bit-identical to one single-GPU launch over the whole frame.
  *
- * Overlap: a run enqueues the exchange on the shard's own communication stream, the two
- * r-row edge bands right behind it on that stream, and at the same time the interior
- * rows [r, own - r) (which read only own rows) on the caller's stream, which then waits
- * for the edges (vip_shard_set_split(h, 1), the default). With split 0 the run filters all own rows in
+ * Overlap: a run enqueues the exchange on the shard's own communication stream and, at
+ * the same time, the interior rows [r, own - r) (which read only own rows) on the
+ * caller's stream; the two r-row edge bands follow once the halos have arrived
+ * (vip_shard_set_split(h, 1), the default). With split 0 the run filters all own rows in
  * one launch after the exchange: fewer launches, and with frames in flight on two streams
  * the exchange of one frame still overlaps the other frame's kernel.
  *
@@ -96,8 +96,8 @@ int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pit
 
 /* As vip_shard_run, with timing events (hipEvent_t, timing enabled, as void*):
  * events[0] before the run on `stream`, events[1] after the exchange on the shard's
- * communication stream, events[2] after the interior rows on `stream` (split mode; else
- * before the launch), events[3] at the end of the run on `stream`. */
+ * communication stream, events[2] after the interior rows on `stream`, events[3] after
+ * the edge bands on `stream`. */
 int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream,
                         void* const* events);
 

@@ -6,8 +6,7 @@
 // communication stream and two events. A run overlaps the halo exchange (RCCL
 // ncclSend/ncclRecv with the two row neighbours, in one group; or device copies for the
 // LOCAL transport) with the interior rows, whose windows stay inside the own rows, and
-// filters the two r-row edge bands once the halos are in, on the communication stream,
-// concurrently with the interior.
+// filters the two r-row edge bands once the halos are in.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -373,10 +372,8 @@ static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
         return rc;
     }
     // exchange first on the communication stream (its kernel is dispatched ahead of the
-    // interior launch) and the edge bands right behind it on the same stream; the interior
-    // on the caller's stream meanwhile, which then waits for the edges. The edges run on
-    // whatever CUs the interior leaves free (a small slab's interior leaves some), or
-    // after it
+    // interior launch), then the interior on the caller's stream, then the edges after
+    // the halos
     if (!rc) rc = (int)hipEventRecord(h->ev_in, s);
     if (!rc) rc = (int)hipStreamWaitEvent(h->comm, h->ev_in, 0);
     if (!rc) {
@@ -386,19 +383,18 @@ static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
         if (!rc) rc = rc2;
     }
     if (!rc) rc = mark(events, 1, h->comm);
+    if (!rc) rc = (int)hipEventRecord(h->ev_x, h->comm);
     if (!h->split) {  // one launch over the own rows once the halos are in
-        if (!rc) rc = (int)hipEventRecord(h->ev_x, h->comm);
         if (!rc) rc = mark(events, 2, s);
         if (!rc) rc = (int)hipStreamWaitEvent(s, h->ev_x, 0);
         if (!rc) rc = filter_rows(h, slab, out, out_pitch, 0, h->own, s);
         if (!rc) rc = mark(events, 3, s);
         return rc;
     }
-    if (!rc) rc = edges(h, slab, out, out_pitch, h->comm);
-    if (!rc) rc = (int)hipEventRecord(h->ev_x, h->comm);  // halos in and edge bands done
     if (!rc) rc = interior(h, slab, out, out_pitch, s);
     if (!rc) rc = mark(events, 2, s);
     if (!rc) rc = (int)hipStreamWaitEvent(s, h->ev_x, 0);
+    if (!rc) rc = edges(h, slab, out, out_pitch, s);
     if (!rc) rc = mark(events, 3, s);
     return rc;
 }
@@ -444,10 +440,8 @@ int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* 
             }
             const int rc2 = group_end(hs, n);
             if (rc || rc2) return rc ? rc : rc2;
-            for (int i = 0; i < n; ++i) {  // edge bands behind the exchange (split mode)
+            for (int i = 0; i < n; ++i) {
                 VIP_HIP_TRY(hipSetDevice(hs[i]->device));
-                if (hs[i]->split)
-                    if (const int e = edges(hs[i], slabs[i], outs[i], out_pitch, hs[i]->comm)) return e;
                 VIP_HIP_TRY(hipEventRecord(hs[i]->ev_x, hs[i]->comm));
             }
         } else {
@@ -464,9 +458,6 @@ int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* 
                     VIP_HIP_TRY(hipMemcpyAsync(slabs[i + 1], slabs[i] + (size_t)h->own * h->pitch(), bytes,
                                                hipMemcpyDeviceToDevice, c));
             }
-            for (int i = 0; i < n; ++i)  // edge bands behind the copies (split mode)
-                if (hs[i]->split)
-                    if (const int e = edges(hs[i], slabs[i], outs[i], out_pitch, c)) return e;
             VIP_HIP_TRY(hipEventRecord(hs[0]->ev_x, c));  // shard 0's event covers the group
         }
         for (int i = 0; i < n; ++i) {
@@ -478,7 +469,8 @@ int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* 
                 continue;
             }
             if (const int rc = interior(hs[i], slabs[i], outs[i], out_pitch, st(i))) return rc;
-            VIP_HIP_TRY(hipStreamWaitEvent(st(i), x, 0));  // halos in and edges done
+            VIP_HIP_TRY(hipStreamWaitEvent(st(i), x, 0));
+            if (const int rc = edges(hs[i], slabs[i], outs[i], out_pitch, st(i))) return rc;
         }
         return 0;
     }
