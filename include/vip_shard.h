@@ -19,12 +19,14 @@
  * reference's replicate border (reads clamp to the own rows), so the sharded result is
  * bit-identical to one single-GPU launch over the whole frame.
  *
- * Overlap: a run enqueues the exchange on the shard's own communication stream and, at
- * the same time, the interior rows [r, own - r) (which read only own rows) on the
- * caller's stream; the two r-row edge bands follow once the halos have arrived
- * (vip_shard_set_split(h, 1), the default). With split 0 the run filters all own rows in
- * one launch after the exchange: fewer launches, and with frames in flight on two streams
- * the exchange of one frame still overlaps the other frame's kernel.
+ * Overlap: with vip_shard_set_split(h, 1) a run enqueues the exchange on the shard's own
+ * communication stream and, at the same time, the interior rows [r, own - r) (which read
+ * only own rows) on the caller's stream; the two r-row edge bands follow once the halos
+ * have arrived. The default (split 0) filters all own rows in one launch after the
+ * exchange: the two edge launches cost more than a small exchange hides (measured on one
+ * MI355X: +11 us per 4K frame at 8 GPUs with two frames in flight, +32 us with one; at
+ * radius 15 an edge launch alone exceeds 100 us), and with frames in flight on two
+ * streams the exchange of one frame overlaps the other frame's kernel anyway.
  *
  * Transports: RCCL (one communicator per rank; ncclSend/ncclRecv between row neighbours
  * in one group, no collective) or LOCAL (all slabs in one process on one device, halos by
@@ -81,8 +83,8 @@ int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* de
                            int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
                            int timeout_ms);
 
-/* 1 (default): interior rows during the exchange, then the two edge bands; 0: one launch
- * over the own rows after the exchange. Same bytes either way. For groups, set it on
+/* 0 (default): one launch over the own rows after the exchange; 1: interior rows during
+ * the exchange, then the two edge bands. Same bytes either way. For groups, set it on
  * every member. */
 int vip_shard_set_split(vip_shard_t h, int split);
 

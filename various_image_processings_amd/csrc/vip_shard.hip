@@ -109,7 +109,7 @@ struct vip_shard_s {
     hipEvent_t ev_in = nullptr;  // own rows written (on the caller's stream)
     hipEvent_t ev_x = nullptr;   // halos received (on comm)
     ncclComm_t nccl = nullptr;   // VIP_SHARD_RCCL
-    int split = 1;               // interior rows under the exchange, then the edge bands
+    int split = 0;               // 1: interior rows under the exchange, then the edge bands
     bool above() const { return rank > 0 && r > 0; }
     bool below() const { return rank < nranks - 1 && r > 0; }
     int slab_rows() const { return own + 2 * r; }

@@ -295,7 +295,7 @@ class NativeShard:
 
     def set_split(self, split: bool) -> None:
         """vip_shard_set_split: interior rows during the exchange, then the edge bands
-        (True, default), or one launch after the exchange (False)."""
+        (True), or one launch after the exchange (False, the default)."""
         from . import _shard_lib as S
         S.call("vip_shard_set_split", self._h, 1 if split else 0)
 
