@@ -481,11 +481,13 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
         if native:
-            def run(i, s=stream, h=0):  # exchange + interior + edges (vip_shard_run)
+            def run(i, s=stream, h=0):  # exchange + filter (vip_shard_run)
                 sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h])
         else:
+            launch = sb.launcher()  # the C entry point with its arguments bound
+
             def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
-                sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h], exchange=False)
+                launch(sp[i % NBUF], dp[i % NBUF], sraw[h])
     res["exchange"] = (None if world == 1 else
                        "native vip_shard (RCCL ncclSend/ncclRecv, overlapped with the interior rows)" if native else
                        f"torch.distributed P2P ({state.get('backend', args.backend)}), serial before the kernel")

@@ -172,20 +172,24 @@ class ShardedBilateral:
         # the handle's height only sizes nothing on the row-band path; use the slab
         self.impl = cls(width, self.geo.slab_rows, ksize, sigma_space, sigma_color, numerics)
         self.adaptive = adaptive
+        self._clamp = self.geo.clamp_range()
 
-    def filter(self, slab, out, stream=None, exchange: bool = True, split: bool = True) -> None:
+    def filter(self, slab, out, stream=None, exchange: bool = True, split: bool = False) -> None:
         """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3).
         exchange and split: the interior rows first (they read no halo), then the halo
         exchange, then the two edge bands (split_bands) -- the kernel's work that can
-        proceed while the halos move is queued ahead of the exchange."""
+        proceed while the halos move is queued ahead of the exchange. Default: the
+        exchange, then one launch (the edge launches cost more than a small exchange
+        hides; vip_shard_set_split)."""
         g = self.geo
-        (i0, ni), edges = split_bands(g)
-        if exchange and split and g.world > 1 and ni > 0:
-            self._rows(slab, out, i0, ni, stream)
-            _exchange_on(slab, g, stream)
-            for e0, ne in edges:
-                self._rows(slab, out, e0, ne, stream)
-            return
+        if exchange and split and g.world > 1:
+            (i0, ni), edges = split_bands(g)
+            if ni > 0:
+                self._rows(slab, out, i0, ni, stream)
+                _exchange_on(slab, g, stream)
+                for e0, ne in edges:
+                    self._rows(slab, out, e0, ne, stream)
+                return
         if exchange:
             _exchange_on(slab, g, stream)
         self._rows(slab, out, 0, g.own, stream)
@@ -194,9 +198,33 @@ class ShardedBilateral:
         """Own rows [row0, row0 + rows) of the slab -> the same rows of out."""
         if rows <= 0:
             return
-        lo, hi = self.geo.clamp_range()
+        lo, hi = self._clamp
         o = out + row0 * self.geo.width * 3 if isinstance(out, int) else out[row0:row0 + rows]
         self.impl.run_rows(slab, o, rows, self.geo.radius + row0, lo, hi, stream=stream)
+
+    def launcher(self):
+        """A lean callable f(slab_ptr, out_ptr, hip_stream) for the whole own-row range
+        (no exchange): the C entry point with every other argument bound, so that a
+        small frame's host cost per launch is the ctypes call alone. Raw device addresses,
+        unchecked (the benchmark's own preallocated buffers)."""
+        from . import _lib
+        g = self.geo
+        lo, hi = self._clamp
+        p = g.width * 3
+        fn = getattr(_lib.lib(), "vip_adaptive_run_rows" if self.adaptive else "vip_bilateral_run_rows")
+        h = self.impl._h
+        name = fn.__name__
+        if self.adaptive:
+            def run(src, dst, stream):
+                rc = fn(h, src, p, dst, p, g.own, g.radius, lo, hi, stream)
+                if rc:
+                    _lib.check(name, rc)
+        else:
+            def run(src, dst, stream):
+                rc = fn(h, src, p, None, 0, dst, p, g.own, g.radius, lo, hi, stream)
+                if rc:
+                    _lib.check(name, rc)
+        return run
 
 
 def texture_halo_rows(ksize: int) -> int:
