@@ -192,7 +192,8 @@ def test_constant_division_is_exact():
     equal the correctly rounded float quotient the reference computes
     (src/bilateral_texture_filter_impl.cu:97-100, :84;
     src/adaptive_bilateral_filter_impl.cu:88-92) for EVERY reachable numerator --
-    checked exhaustively here (texture ksize 2..17, adaptive ksize up to 31)."""
+    checked exhaustively here (texture ksize 2..24 and beyond, windows 2*(k//2)+1 wide for
+    even k too; adaptive ksize up to 31 -- above, the runtime-radius kernel divides in IEEE)."""
     cases = [((2 * (k // 2) + 1) ** 2 * 255, k * k) for k in range(2, 32)] + [(765, 3)]
     for smax, d in cases:
         s = np.arange(smax + 1, dtype=np.float32)
