@@ -481,8 +481,10 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
         if native:
+            nrun = sb.launcher()  # vip_shard_run with its arguments bound
+
             def run(i, s=stream, h=0):  # exchange + filter (vip_shard_run)
-                sb.filter(sp[i % NBUF], dp[i % NBUF], stream=sraw[h])
+                nrun(sp[i % NBUF], dp[i % NBUF], sraw[h])
         else:
             launch = sb.launcher()  # the C entry point with its arguments bound
 

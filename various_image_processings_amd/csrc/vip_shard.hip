@@ -214,7 +214,8 @@ int enqueue_p2p(const vip_shard_s* h, uint8_t* slab) {
 
 int group_end(vip_shard_s* const* hs, int n) {
     const ncclResult_t e = ncclGroupEnd();
-    if (e != ncclSuccess && e != ncclInProgress) return comm_fail(e, "ncclGroupEnd");
+    if (e == ncclSuccess) return 0;  // enqueued (blocking communicators)
+    if (e != ncclInProgress) return comm_fail(e, "ncclGroupEnd");
     for (int i = 0; i < n; ++i)
         if (const int rc = wait_comm(hs[i]->nccl, hs[i]->timeout_ms, "halo exchange")) return rc;
     return 0;

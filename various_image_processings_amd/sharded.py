@@ -335,6 +335,20 @@ class NativeShard:
         S.call("vip_shard_run", self._h, _ptr(slab, p * self.geo.slab_rows), _ptr(out, p * self.geo.own), p,
                _stream(stream))
 
+    def launcher(self):
+        """A lean callable f(slab_ptr, out_ptr, hip_stream) for vip_shard_run with the
+        handle and pitch bound (raw device addresses, unchecked): the host cost per frame
+        is the ctypes call, which matters when a rank's slab takes ~25 us on the GPU."""
+        from . import _shard_lib as S
+        fn = S.lib().vip_shard_run
+        h, p = self._h, self.geo.width * 3
+
+        def run(slab, out, stream):
+            rc = fn(h, slab, out, p, stream)
+            if rc:
+                raise S.ShardError("vip_shard_run", rc)
+        return run
+
     def filter_timed(self, slab, out, events, stream=None) -> None:
         """events: 4 timing-enabled torch.cuda.Event (vip_shard_run_timed): run start,
         halos received (communication stream), interior done, edges done."""
