@@ -124,6 +124,8 @@ def parse():
     # control), "torch" = torch.distributed P2P before the kernel. Default native, torch for
     # the one-GPU gloo rehearsal and the texture filter.
     p.add_argument("--exchange", default=None, choices=["native", "torch"])
+    # rehearsal of the N > 1 native path in ONE process (a one-rank RCCL communicator)
+    p.add_argument("--rehearse-native", action="store_true")
     return p.parse_args()
 
 
@@ -435,6 +437,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     res = dict(frame_h=frame_h, exchange=None, stage_ms=None, samples=None)
     native = False
     cdev = dev if state.get("backend") == "nccl" else "cpu"  # control tensors of the process group
+    multi = state.get("multi", world > 1)  # a process group is up (N > 1, or --rehearse-native)
 
     if cfg["kind"] == "texture" and world == 1:
         rows = frame_h
@@ -471,7 +474,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             sts[h].filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
     else:
         ns = None
-        if world > 1 and args.exchange == "native":
+        if multi and args.exchange == "native":
             ns, why = native_shard(args, cfg, frame_h, rank, world)
             if ns is None:  # fall back to torch.distributed P2P over a new RCCL group
                 if "torch_group" not in state:
@@ -495,7 +498,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
 
             def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
                 launch(sp[i % NBUF], dp[i % NBUF], sraw[h])
-    res["exchange"] = (None if world == 1 else
+    res["exchange"] = (None if not multi else
                        "native vip_shard (RCCL ncclSend/ncclRecv, overlapped with the interior rows)" if native else
                        f"torch.distributed P2P ({state.get('backend', args.backend)}), serial before the kernel")
 
@@ -540,7 +543,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     # (the ranks must issue the same P2P sequence), so the settle runs a step count
     # agreed by rank 0.
     t_settle, i_settle = time.perf_counter(), 0
-    if world == 1:
+    if not multi:
         while time.perf_counter() - t_settle < args.settle_s:
             for _ in range(8):
                 run(i_settle, streams[i_settle % S], i_settle % S)
@@ -609,7 +612,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     after = base + args.warmup + args.steps
     single_ms = None
     parts = None
-    if world > 1:
+    if multi:
         for i in range(max(4, args.steps // 4)):
             step(after + i, sample=True)
         torch.cuda.synchronize(dev)
@@ -654,7 +657,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     keys = ["elapsed", "launch"] + (sorted(parts) if parts else [])
     vals = [elapsed, launch_ms] + ([parts[x] for x in sorted(parts)] if parts else [])
     t = torch.tensor(vals, dtype=torch.float64, device=cdev)
-    if world > 1:
+    if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     got = dict(zip(keys, (float(v) for v in t)))
     res.update(elapsed=got["elapsed"], launch_ms=got["launch"], frame_ms=kernel_ms, rows=rows, geo=geo,
@@ -691,8 +694,18 @@ def main():
         args.exchange = "torch"  # the texture filter's wide halo goes through ShardedTexture
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    state = {}
-    if world > 1:
+    state = {"multi": world > 1 or args.rehearse_native}
+    if args.rehearse_native:
+        # one rank through the N > 1 native path (a one-rank RCCL communicator, no
+        # neighbours): id broadcast, vip_shard_create, the split timing, the evented steps
+        if world != 1:
+            raise SystemExit("--rehearse-native is a single-process run")
+        args.exchange = "native"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29400 + os.getpid() % 500))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if state["multi"]:
         state["backend"] = init_distributed(args, rank, dev)
 
     import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
@@ -774,7 +787,7 @@ def main():
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows, "data": args.data,
                    "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
                    **({"texture_mode": args.texture_mode} if cfg["kind"] == "texture" and world == 1 else {}),
-                   **({"backend": state.get("backend"), "exchange": m["exchange"]} if world > 1 else {}),
+                   **({"backend": state.get("backend"), "exchange": m["exchange"]} if state["multi"] else {}),
                    **({"exchange_fallback": m["exchange_fallback"]} if m.get("exchange_fallback") else {})},
         "roofline": roof,
         # per step, max over ranks: one frame on one stream (N>1: with its exchange),
@@ -797,7 +810,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if state["multi"]:
         dist.destroy_process_group()
 
 

@@ -5,6 +5,9 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the N > 1 native bench path in one process (one-rank RCCL communicator)
+timeout -k 10 200 python bench.py --config c2 --rehearse-native --steps 200 --no-cpu-baseline > gpurun_out/r03_native_rehearsal.json 2> gpurun_out/b_nat.err
+rc=$?; echo "native rehearsal rc=$rc"; cat gpurun_out/r03_native_rehearsal.json | grep -v Gloo; [ $rc -eq 0 ] || { tail -20 gpurun_out/b_nat.err; exit $rc; }
 timeout -k 10 300 python bench.py --config k65 > gpurun_out/r03_k65_bench.json 2> gpurun_out/b_k65.err
 rc=$?; echo "bench k65 rc=$rc"; cut -c1-400 gpurun_out/r03_k65_bench.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/b_k65.err; exit $rc; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_k65 -o run --output-format csv -- python bench.py --config k65 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/prof_k65.log 2>&1
