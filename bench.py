@@ -568,8 +568,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         # exchange's latency on this machine: time both (max over ranks) and keep the faster.
         trial = {}
         n_trial = 40
-        for sp in (True, False):
-            sb.set_split(sp)
+        for split in (True, False):
+            sb.set_split(split)
             torch.cuda.synchronize(dev)
             dist.barrier()
             t0 = time.perf_counter()
@@ -580,7 +580,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             dist.barrier()
             dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            trial[sp] = float(dt[0])
+            trial[split] = float(dt[0])
         best = min(trial, key=trial.get)
         sb.set_split(best)
         res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best
