@@ -10,5 +10,5 @@ hipcc $F -c vip_texture.hip -o /tmp/tvar_$name/t.o
 # every other object from the in-place CMake build (__graft_entry__.build())
 O=../../build/cmake/CMakeFiles
 hipcc --offload-arch=gfx950 -shared -o ../../variants/$name.so /tmp/tvar_$name/t.o \
-  $(ls $O/vip_{bil,ada,capi}*.dir/various_image_processings_amd/csrc/*.o $O/vip_hip.dir/various_image_processings_amd/csrc/*.o)
+  $(ls $O/vip_{bil,ada,capi,stencil_rt}*.dir/various_image_processings_amd/csrc/*.o $O/vip_hip.dir/various_image_processings_amd/csrc/*.o)
 echo built variants/$name.so

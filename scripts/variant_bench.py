@@ -40,7 +40,10 @@ if "--r15" in sys.argv:  # one 2048-row slab of the C5 frame (16384 wide, ksize 
     b31 = _BilateralImpl(16384, 2048 + 30, 31)
     cases += [("bilateral_r15_slab", lambda s, d: b31.bilateral_filter(s15[0], d15))]
 import time
+only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
 for name, f in cases:
+    if only and not any(name.startswith(o) for o in only):
+        continue
     # clock settle: 1 s of back-to-back launches (MI355X clocks ramp under sustained load)
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 1.0:

@@ -831,6 +831,10 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int 
 template <bool CPP>
 static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
                        int aligned, hipStream_t s) {
+#ifdef VIP_GF_ONLY_R2  // quick variant builds (scripts/build_texture_variant.sh): k = 4, 5 only
+    if (ksize / 2 == 2) return launch_gf<2, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+    return VIP_ERR_UNSUPPORTED_KSIZE;
+#endif
     switch (ksize / 2) {  // ksize 1..24 (kMaxKsizeTexture)
         case 1: return launch_gf<1, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
         case 2: return launch_gf<2, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
