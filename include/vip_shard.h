@@ -13,7 +13,8 @@
  * [row_begin, row_begin + own) of a frame_height-row frame (balanced contiguous split, the
  * first frame_height % nranks ranks one row more). Its slab is a dense (own + 2r) x width
  * RGB8 buffer (pitch width * 3): rows [0, r) halo above, [r, r + own) own rows,
- * [r + own, 2r + own) halo below, r = ksize / 2. The caller fills the own rows; a run
+ * [r + own, 2r + own) halo below, r = ksize / 2 (texture: see below; vip_shard_geometry
+ * returns r). The caller fills the own rows; a run
  * receives the halos from the row neighbours, then filters the own rows into `out`
  * (own rows, any pitch). At the first / last rank the missing halo is replaced by the
  * reference's replicate border (reads clamp to the own rows), so the sharded result is
@@ -61,6 +62,15 @@ extern "C" {
 
 typedef struct vip_shard_s* vip_shard_t;
 
+/* Texture filter shards (VIP_FILTER_TEXTURE; vip_shard_create_texture /
+ * vip_shard_create_group_texture): the halo is nitr * vip_texture_halo_rows(ksize) rows
+ * (45 at k = 5, nitr = 5), exchanged ONCE per frame; iteration t then filters the own
+ * rows plus (nitr - 1 - t) * vip_texture_halo_rows(ksize) rows on each side (a ghost zone
+ * that shrinks to the own rows), so the result equals one single-GPU vip_texture_run of
+ * the whole frame, bit for bit, with one exchange instead of nitr. The shard holds two
+ * extra slabs for the iterations. No interior/edge split (every iteration reads the halo
+ * region): vip_shard_set_split(h, 1) returns VIP_ERR_INVALID_ARGUMENT. */
+
 /* Balanced contiguous row split: rank's first row and row count (no device call). */
 int vip_shard_rows(int frame_height, int nranks, int rank, int* row_begin, int* own_rows);
 
@@ -76,12 +86,21 @@ int vip_shard_unique_id(void* id);
 int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
                      float sigma_color, int numerics, int nranks, int rank, const void* id, int timeout_ms);
 
+/* vip_shard_create for the bilateral texture filter (CudaBilateralTextureFilter's ksize
+ * 1..24 and nitr >= 0). */
+int vip_shard_create_texture(vip_shard_t* out, int width, int frame_height, int ksize, int nitr, int numerics,
+                             int nranks, int rank, const void* id, int timeout_ms);
+
 /* One process, n shards: transport VIP_SHARD_RCCL puts shard i on devices[i] (one RCCL
  * communicator per device, initialised together -- ncclCommInitAll's pattern);
  * VIP_SHARD_LOCAL puts all n on the current device (devices ignored). out[n]. */
 int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* devices, int kind, int width,
                            int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
                            int timeout_ms);
+
+/* vip_shard_create_group for the bilateral texture filter. */
+int vip_shard_create_group_texture(vip_shard_t* out, int n, int transport, const int* devices, int width,
+                                   int frame_height, int ksize, int nitr, int numerics, int timeout_ms);
 
 /* 0 (default): one launch over the own rows after the exchange; 1: interior rows during
  * the exchange, then the two edge bands. Same bytes either way. For groups, set it on

@@ -5,9 +5,10 @@
 // The reference has no multi-device code; this is what a C++ caller of
 // vip_bilateral_run_rows would otherwise write by hand.
 //
-// usage: vip_shard_frame [width height ksize] [steps] [--local N] [--adaptive]
+// usage: vip_shard_frame [width height ksize] [steps] [--local N] [--adaptive | --texture NITR]
 //   default 16384 16384 31, 10 timed steps; --local N: N shards on device 0 (halos by
-//   device copies), the same code path on a single GPU.
+//   device copies), the same code path on a single GPU; --texture NITR: the bilateral
+//   texture filter with k = ksize (one nitr-deep halo exchange per frame).
 // The frame is mt19937(42) % 255 per byte (test/random_array.hpp's generator); each
 // device gets its own rows, the sharded output is gathered and compared byte for byte
 // with one whole-frame launch on device 0. Prints Mpixels/s over the timed steps (host
@@ -36,19 +37,21 @@
     } while (0)
 
 int main(int argc, char** argv) {
-    int local = 0;
+    int local = 0, nitr = -1;
     bool adaptive = false;
     std::vector<std::string> pos;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--local") && i + 1 < argc) local = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--adaptive")) adaptive = true;
+        else if (!std::strcmp(argv[i], "--texture") && i + 1 < argc) nitr = std::atoi(argv[++i]);
         else pos.push_back(argv[i]);
     }
     const int width = pos.size() >= 3 ? std::atoi(pos[0].c_str()) : 16384;
     const int height = pos.size() >= 3 ? std::atoi(pos[1].c_str()) : 16384;
     const int ksize = pos.size() >= 3 ? std::atoi(pos[2].c_str()) : 31;
     const int steps = pos.size() >= 4 ? std::atoi(pos[3].c_str()) : (pos.size() == 1 ? std::atoi(pos[0].c_str()) : 10);
-    const int kind = adaptive ? VIP_FILTER_ADAPTIVE : VIP_FILTER_BILATERAL;
+    const bool texture = nitr >= 0;
+    const int kind = texture ? VIP_FILTER_TEXTURE : adaptive ? VIP_FILTER_ADAPTIVE : VIP_FILTER_BILATERAL;
     int ndev = 0;
     CHECK(vip_device_count(&ndev));
     const int n = local > 0 ? local : ndev;
@@ -56,7 +59,8 @@ int main(int argc, char** argv) {
     std::vector<int> devs(n);
     for (int i = 0; i < n; ++i) devs[i] = local > 0 ? 0 : i;
     std::printf("frame %dx%d ksize %d %s, %d shard(s) on %s\n", width, height, ksize,
-                adaptive ? "adaptive" : "bilateral", n, local > 0 ? "device 0 (LOCAL transport)" : "one GPU each (RCCL)");
+                texture ? "texture" : adaptive ? "adaptive" : "bilateral", n,
+                local > 0 ? "device 0 (LOCAL transport)" : "one GPU each (RCCL)");
 
     const size_t pitch = (size_t)width * 3;
     std::vector<uint8_t> frame(pitch * height);
@@ -65,8 +69,12 @@ int main(int argc, char** argv) {
 
     CHECK(vip_set_device(devs[0]));
     std::vector<vip_shard_t> hs(n);
-    CHECK(vip_shard_create_group(hs.data(), n, transport, devs.data(), kind, width, height, ksize, 10.f, 30.f,
-                                 VIP_NUMERICS_CUDA, 120000));
+    if (texture)
+        CHECK(vip_shard_create_group_texture(hs.data(), n, transport, devs.data(), width, height, ksize, nitr,
+                                             VIP_NUMERICS_CUDA, 120000));
+    else
+        CHECK(vip_shard_create_group(hs.data(), n, transport, devs.data(), kind, width, height, ksize, 10.f, 30.f,
+                                     VIP_NUMERICS_CUDA, 120000));
     std::vector<uint8_t*> slabs(n), outs(n);
     std::vector<void*> streams(n);
     std::vector<int> own(n), begin(n);
@@ -103,7 +111,13 @@ int main(int argc, char** argv) {
     CHECK(vip_malloc(reinterpret_cast<void**>(&d_src), frame.size()));
     CHECK(vip_malloc(reinterpret_cast<void**>(&d_dst), frame.size()));
     CHECK(vip_upload(d_src, frame.data(), frame.size()));
-    if (adaptive) {
+    if (texture) {
+        vip_texture_t t = nullptr;
+        CHECK(vip_texture_create(&t, width, height, ksize, nitr, VIP_NUMERICS_CUDA));
+        CHECK(vip_texture_run(t, d_src, d_dst, nullptr));
+        CHECK(vip_device_synchronize());
+        vip_texture_destroy(t);
+    } else if (adaptive) {
         vip_adaptive_t a = nullptr;
         CHECK(vip_adaptive_create(&a, width, height, ksize, 10.f, 30.f, VIP_NUMERICS_CUDA));
         CHECK(vip_adaptive_run(a, d_src, pitch, d_dst, pitch, nullptr));

@@ -6,7 +6,8 @@ Sharded output must equal one single-GPU launch over the whole frame, bit for bi
   the same stream ordering as the RCCL transport;
 * RCCL transport with one rank (no neighbours; a one-device communicator), both as a
   one-process group and through the multi-process entry point with a unique id;
-* a communicator whose peer never joins returns VIP_ERR_COMM_TIMEOUT, no hang.
+* a communicator whose peer never joins returns VIP_ERR_COMM_TIMEOUT, no hang;
+* the texture filter (vip_shard_create_*_texture): one nitr-deep exchange per frame.
 A multi-rank RCCL exchange needs several GPUs: it runs in the driver's 8-GPU bench.
 """
 import os
@@ -23,21 +24,24 @@ from various_image_processings_amd.sharded import NativeShard, ShardGroup, nativ
 pytestmark = pytest.mark.gpu
 
 
-def _single(dev, img, k, adaptive):
+def _single(dev, img, k, adaptive, nitr=None):
     h, w, _ = img.shape
     d = dev.empty((h, w, 3))
-    if adaptive:
+    if nitr is not None:
+        vip.CudaBilateralTextureFilter(w, h, k, nitr).execute(dev.put(img), d)
+    elif adaptive:
         vip.CudaAdaptiveBilateralFilter(w, h, k).execute(dev.put(img), d)
     else:
         vip.CudaBilateralFilter(w, h, k).bilateral_filter(dev.put(img), d)
     return dev.get(d)
 
 
-def _run_group(dev, img, k, n, adaptive, transport=S.VIP_SHARD_LOCAL, devices=None, split=True):
+def _run_group(dev, img, k, n, adaptive, transport=S.VIP_SHARD_LOCAL, devices=None, split=True, nitr=None):
     torch = dev.torch_
     h, w, _ = img.shape
-    g = ShardGroup(n, w, h, k, transport=transport, devices=devices, adaptive=adaptive)
-    g.set_split(split)
+    g = ShardGroup(n, w, h, k, transport=transport, devices=devices, adaptive=adaptive, nitr=nitr)
+    if nitr is None:
+        g.set_split(split)
     slabs, outs, streams = [], [], []
     for geo in g.geos:
         b, e = geo.rows
@@ -77,6 +81,51 @@ def test_local_group_c5_frame_8_way(dev, oracle):
     """C5's ksize 31 over a 16384-wide frame, 8 slabs: every pixel equals one launch."""
     img = oracle.random_image(16384, 2048)
     assert np.array_equal(_run_group(dev, img, 31, 8, False), _single(dev, img, 31, False))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_local_group_texture_equals_single_run_4k(dev, oracle, n):
+    """The texture filter row-sharded natively (vip_shard_create_group_texture): one
+    45-row halo exchange per frame (k = 5, nitr = 5), a shrinking ghost zone over the
+    iterations; every pixel equals one vip_texture_run of the whole 4K frame."""
+    img = oracle.random_image(3840, 2160)
+    assert np.array_equal(_run_group(dev, img, 5, n, False, nitr=5), _single(dev, img, 5, False, nitr=5))
+
+
+@pytest.mark.parametrize("shape,k,nitr,n", [((301, 173), 5, 3, 3), ((200, 150), 4, 2, 2), ((90, 120), 3, 1, 4),
+                                            ((64, 80), 5, 0, 2), ((130, 97), 9, 2, 2)])
+def test_local_group_texture_vs_oracle(dev, oracle, shape, k, nitr, n):
+    """Ragged frames, an even k, one iteration, nitr = 0 (the source), against the oracle."""
+    h, w = shape
+    img = oracle.random_u8(h * w * 3).reshape(h, w, 3)
+    assert np.array_equal(_run_group(dev, img, k, n, False, nitr=nitr), oracle.texture(img, k, nitr))
+
+
+def test_texture_shard_has_no_split(dev):
+    g = ShardGroup(2, 256, 200, 5, nitr=2)
+    assert g.geos[0].radius == 2 * 9
+    with pytest.raises(vip.VipError) as e:
+        g.set_split(True)
+    assert e.value.code == 10001
+    with pytest.raises(vip.VipError):
+        ShardGroup(8, 256, 300, 5, nitr=5)  # 37-row shards < 45-row halo
+
+
+def test_rccl_texture_single_rank(dev, oracle):
+    """vip_shard_create_texture with a unique id, nranks = 1, and a one-device group."""
+    import torch
+    img = oracle.random_image(700, 400)
+    want = _single(dev, img, 5, False, nitr=3)
+    s = NativeShard(700, 400, 5, 0, 1, native_unique_id(), nitr=3)
+    geo = s.geo
+    slab = dev.empty((geo.slab_rows, 700, 3))
+    slab[geo.radius:geo.radius + geo.own] = dev.put(img)
+    out = dev.empty((400, 700, 3))
+    s.filter(slab, out)
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.get(out), want)
+    got = _run_group(dev, img, 5, 1, False, transport=S.VIP_SHARD_RCCL, devices=[torch.cuda.current_device()], nitr=3)
+    assert np.array_equal(got, want)
 
 
 def test_thin_shards_rejected_before_any_device_work(dev):
@@ -143,7 +192,8 @@ os._exit(0)  # RCCL's bootstrap thread still waits for the missing rank: leave w
 
 
 @pytest.mark.parametrize("argv", [["4096", "2048", "31", "2", "--local", "8"], ["3840", "2160", "15", "3"],
-                                  ["2000", "999", "63", "1", "--local", "3", "--adaptive"]])
+                                  ["2000", "999", "63", "1", "--local", "3", "--adaptive"],
+                                  ["3840", "2160", "5", "2", "--local", "4", "--texture", "5"]])
 def test_shard_frame_sample(dev, argv):
     """samples/vip_shard_frame (a C++ caller of vip_shard.h): the sharded frame gathered
     from its shards equals one whole-frame launch (exit status 0, 'equals')."""

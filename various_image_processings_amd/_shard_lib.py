@@ -26,7 +26,9 @@ SIGNATURES = {
     "vip_shard_rows": (_i, [_i, _i, _i, _ip, _ip]),
     "vip_shard_unique_id": (_i, [_p]),
     "vip_shard_create": (_i, [_pp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _p, _i]),
+    "vip_shard_create_texture": (_i, [_pp, _i, _i, _i, _i, _i, _i, _i, _p, _i]),
     "vip_shard_create_group": (_i, [_pp, _i, _i, _ip, _i, _i, _i, _i, _f, _f, _i, _i]),
+    "vip_shard_create_group_texture": (_i, [_pp, _i, _i, _ip, _i, _i, _i, _i, _i, _i]),
     "vip_shard_geometry": (_i, [_p, _ip, _ip, _ip]),
     "vip_shard_set_split": (_i, [_p, _i]),
     "vip_shard_run": (_i, [_p, _p, _p, _s, _p]),

@@ -105,6 +105,9 @@ struct vip_shard_s {
     int row_begin, own, r;
     vip_bilateral_t bil = nullptr;
     vip_adaptive_t ada = nullptr;
+    vip_texture_t tex = nullptr;           // VIP_FILTER_TEXTURE: nitr iterations, ghost zone
+    int nitr = 0, step = 0;                // iterations; rows one iteration reaches (halo = nitr * step)
+    uint8_t* scratch[2] = {nullptr, nullptr};  // texture: ping-pong slabs between iterations
     hipStream_t comm = nullptr;  // halo exchange stream
     hipEvent_t ev_in = nullptr;  // own rows written (on the caller's stream)
     hipEvent_t ev_x = nullptr;   // halos received (on comm)
@@ -120,14 +123,29 @@ extern "C" int vip_shard_destroy(vip_shard_t h);
 
 namespace {
 
+// What every rank's shard filters (the create functions' arguments).
+struct FilterSpec {
+    int kind, ksize;
+    float sigma_space, sigma_color;  // bilateral, adaptive
+    int nitr;                        // texture
+    int numerics;
+};
+
 // Filter handle, stream and events of a shard on the current device (geometry set).
-int init_shard(vip_shard_s* h, float sigma_space, float sigma_color) {
+int init_shard(vip_shard_s* h, const FilterSpec& f) {
     VIP_HIP_TRY(hipGetDevice(&h->device));
-    int rc = h->kind == VIP_FILTER_ADAPTIVE
-                 ? vip_adaptive_create(&h->ada, h->width, h->slab_rows(), h->ksize, sigma_space, sigma_color,
-                                       h->numerics)
-                 : vip_bilateral_create(&h->bil, h->width, h->slab_rows(), h->ksize, sigma_space, sigma_color,
-                                        h->numerics);
+    int rc = 0;
+    if (h->kind == VIP_FILTER_TEXTURE) {
+        rc = vip_texture_create(&h->tex, h->width, h->slab_rows(), h->ksize, h->nitr, h->numerics);
+        for (int i = 0; i < 2 && !rc && h->nitr > 1; ++i)
+            rc = (int)hipMalloc(reinterpret_cast<void**>(&h->scratch[i]), (size_t)h->slab_rows() * h->pitch());
+    } else if (h->kind == VIP_FILTER_ADAPTIVE) {
+        rc = vip_adaptive_create(&h->ada, h->width, h->slab_rows(), h->ksize, f.sigma_space, f.sigma_color,
+                                 h->numerics);
+    } else {
+        rc = vip_bilateral_create(&h->bil, h->width, h->slab_rows(), h->ksize, f.sigma_space, f.sigma_color,
+                                  h->numerics);
+    }
     if (rc) return rc;
     VIP_HIP_TRY(hipStreamCreateWithFlags(&h->comm, hipStreamNonBlocking));
     VIP_HIP_TRY(hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming));
@@ -138,21 +156,35 @@ int init_shard(vip_shard_s* h, float sigma_space, float sigma_color) {
 // Geometry shared by every rank (sharded.py SlabGeometry); VIP_ERR_INVALID_ARGUMENT when
 // the thinnest shard cannot cover a halo (checked identically on every rank, before any
 // communication, so no rank is left waiting in an exchange the others never join).
-int new_shard(vip_shard_s** out, int kind, int width, int frame_height, int ksize, int numerics, int nranks, int rank,
+// The texture filter's halo is nitr iterations deep (sharded.py ShardedTexture): one
+// exchange per frame, then iteration t filters the own rows plus (nitr - 1 - t) * step
+// rows on each side, so the last iteration's own rows are exact.
+int new_shard(vip_shard_s** out, const FilterSpec& f, int width, int frame_height, int nranks, int rank,
               int transport, int timeout_ms) {
     if (!out || width <= 0 || frame_height <= 0 || nranks <= 0 || rank < 0 || rank >= nranks)
         return VIP_ERR_INVALID_ARGUMENT;
-    if (kind != VIP_FILTER_BILATERAL && kind != VIP_FILTER_ADAPTIVE) return VIP_ERR_INVALID_ARGUMENT;
-    if (ksize < 1 || !(ksize & 1)) return VIP_ERR_UNSUPPORTED_KSIZE;
-    const int r = ksize / 2;
+    int r = 0, step = 0;
+    if (f.kind == VIP_FILTER_TEXTURE) {
+        if (f.ksize < 1) return VIP_ERR_UNSUPPORTED_KSIZE;  // the texture handle checks the upper limit
+        if (f.nitr < 0) return VIP_ERR_INVALID_ARGUMENT;
+        step = vip_texture_halo_rows(f.ksize);
+        r = f.nitr * step;
+    } else if (f.kind == VIP_FILTER_BILATERAL || f.kind == VIP_FILTER_ADAPTIVE) {
+        if (f.ksize < 1 || !(f.ksize & 1)) return VIP_ERR_UNSUPPORTED_KSIZE;
+        r = f.ksize / 2;
+    } else {
+        return VIP_ERR_INVALID_ARGUMENT;
+    }
     if (nranks > 1 && frame_height / nranks < r) return VIP_ERR_INVALID_ARGUMENT;
     auto* h = new (std::nothrow) vip_shard_s();
     if (!h) return (int)hipErrorOutOfMemory;
-    h->kind = kind;
+    h->kind = f.kind;
     h->width = width;
     h->frame_height = frame_height;
-    h->ksize = ksize;
-    h->numerics = numerics;
+    h->ksize = f.ksize;
+    h->numerics = f.numerics;
+    h->nitr = f.nitr;
+    h->step = step;
     h->nranks = nranks;
     h->rank = rank;
     h->transport = transport;
@@ -170,10 +202,33 @@ void clamp_range(const vip_shard_s* h, int* lo, int* hi) {
     *hi = h->below() ? h->slab_rows() : h->r + h->own;
 }
 
+// Texture: all own rows, nitr iterations with a shrinking ghost zone (the halos must be in).
+int texture_rows(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pitch, hipStream_t s) {
+    int lo, hi;
+    clamp_range(h, &lo, &hi);
+    if (h->nitr == 0)  // the reference's execute with nitr = 0 returns the source
+        return (int)hipMemcpy2DAsync(out, out_pitch, slab + (size_t)h->r * h->pitch(), h->pitch(), h->pitch(),
+                                     h->own, hipMemcpyDeviceToDevice, s);
+    const uint8_t* a = slab;
+    for (int t = 0; t < h->nitr; ++t) {
+        if (t == h->nitr - 1)
+            return vip_texture_iterate_rows(h->tex, a, out, out_pitch, h->r, h->own, lo, hi, s);
+        const int m = (h->nitr - 1 - t) * h->step;
+        const int r0 = h->r - m > lo ? h->r - m : lo, r1 = h->r + h->own + m < hi ? h->r + h->own + m : hi;
+        uint8_t* b = h->scratch[t % 2];
+        if (const int rc = vip_texture_iterate_rows(h->tex, a, b + (size_t)r0 * h->pitch(), h->pitch(), r0, r1 - r0,
+                                                    lo, hi, s))
+            return rc;
+        a = b;
+    }
+    return 0;
+}
+
 // Own rows [row0, row0 + n) of the slab -> the same rows of out.
 int filter_rows(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pitch, int row0, int n,
                 hipStream_t s) {
     if (n <= 0) return 0;
+    if (h->kind == VIP_FILTER_TEXTURE) return texture_rows(h, slab, out, out_pitch, s);  // row0 = 0, n = own
     int lo, hi;
     clamp_range(h, &lo, &hi);
     uint8_t* o = out + (size_t)row0 * out_pitch;
@@ -258,13 +313,13 @@ int vip_shard_unique_id(void* id) {
 
 const char* vip_shard_last_error(void) { return g_last_error.c_str(); }
 
-int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
-                     float sigma_color, int numerics, int nranks, int rank, const void* id, int timeout_ms) {
+static int create_rank(vip_shard_t* out, const FilterSpec& f, int width, int frame_height, int nranks, int rank,
+                       const void* id, int timeout_ms) {
     if (!out || !id) return VIP_ERR_INVALID_ARGUMENT;
     vip_shard_s* h = nullptr;
-    int rc = new_shard(&h, kind, width, frame_height, ksize, numerics, nranks, rank, VIP_SHARD_RCCL, timeout_ms);
+    int rc = new_shard(&h, f, width, frame_height, nranks, rank, VIP_SHARD_RCCL, timeout_ms);
     if (rc) return rc;
-    rc = init_shard(h, sigma_space, sigma_color);
+    rc = init_shard(h, f);
     if (!rc) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
@@ -294,18 +349,17 @@ int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, in
     return 0;
 }
 
-int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* devices, int kind, int width,
-                           int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
-                           int timeout_ms) {
+static int create_group(vip_shard_t* out, int n, int transport, const int* devices, const FilterSpec& f, int width,
+                        int frame_height, int timeout_ms) {
     if (!out || n <= 0 || (transport != VIP_SHARD_RCCL && transport != VIP_SHARD_LOCAL)) return VIP_ERR_INVALID_ARGUMENT;
     if (transport == VIP_SHARD_RCCL && !devices) return VIP_ERR_INVALID_ARGUMENT;
     DeviceGuard guard;
     for (int i = 0; i < n; ++i) out[i] = nullptr;
     int rc = 0;
     for (int i = 0; i < n && !rc; ++i) {
-        rc = new_shard(&out[i], kind, width, frame_height, ksize, numerics, n, i, transport, timeout_ms);
+        rc = new_shard(&out[i], f, width, frame_height, n, i, transport, timeout_ms);
         if (!rc && transport == VIP_SHARD_RCCL) rc = (int)hipSetDevice(devices[i]);
-        if (!rc) rc = init_shard(out[i], sigma_space, sigma_color);
+        if (!rc) rc = init_shard(out[i], f);
     }
     if (!rc && transport == VIP_SHARD_RCCL) {
         // one communicator per device, initialised in one group (ncclCommInitAll's pattern)
@@ -344,8 +398,36 @@ int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* de
     return rc;
 }
 
+int vip_shard_create(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
+                     float sigma_color, int numerics, int nranks, int rank, const void* id, int timeout_ms) {
+    if (kind != VIP_FILTER_BILATERAL && kind != VIP_FILTER_ADAPTIVE) return VIP_ERR_INVALID_ARGUMENT;
+    return create_rank(out, FilterSpec{kind, ksize, sigma_space, sigma_color, 0, numerics}, width, frame_height,
+                       nranks, rank, id, timeout_ms);
+}
+
+int vip_shard_create_texture(vip_shard_t* out, int width, int frame_height, int ksize, int nitr, int numerics,
+                             int nranks, int rank, const void* id, int timeout_ms) {
+    return create_rank(out, FilterSpec{VIP_FILTER_TEXTURE, ksize, 0.f, 0.f, nitr, numerics}, width, frame_height,
+                       nranks, rank, id, timeout_ms);
+}
+
+int vip_shard_create_group(vip_shard_t* out, int n, int transport, const int* devices, int kind, int width,
+                           int frame_height, int ksize, float sigma_space, float sigma_color, int numerics,
+                           int timeout_ms) {
+    if (kind != VIP_FILTER_BILATERAL && kind != VIP_FILTER_ADAPTIVE) return VIP_ERR_INVALID_ARGUMENT;
+    return create_group(out, n, transport, devices, FilterSpec{kind, ksize, sigma_space, sigma_color, 0, numerics},
+                        width, frame_height, timeout_ms);
+}
+
+int vip_shard_create_group_texture(vip_shard_t* out, int n, int transport, const int* devices, int width,
+                                   int frame_height, int ksize, int nitr, int numerics, int timeout_ms) {
+    return create_group(out, n, transport, devices, FilterSpec{VIP_FILTER_TEXTURE, ksize, 0.f, 0.f, nitr, numerics},
+                        width, frame_height, timeout_ms);
+}
+
 int vip_shard_set_split(vip_shard_t h, int split) {
     if (!h || (split != 0 && split != 1)) return VIP_ERR_INVALID_ARGUMENT;
+    if (split && h->kind == VIP_FILTER_TEXTURE) return VIP_ERR_INVALID_ARGUMENT;  // every iteration needs the halos
     h->split = split;
     return 0;
 }
@@ -495,6 +577,9 @@ int vip_shard_destroy(vip_shard_t h) {
     }
     if (h->bil) vip_bilateral_destroy(h->bil);
     if (h->ada) vip_adaptive_destroy(h->ada);
+    if (h->tex) vip_texture_destroy(h->tex);
+    for (uint8_t* p : h->scratch)
+        if (p) (void)hipFree(p);
     if (h->comm) (void)hipStreamDestroy(h->comm);
     if (h->ev_in) (void)hipEventDestroy(h->ev_in);
     if (h->ev_x) (void)hipEventDestroy(h->ev_x);

@@ -307,19 +307,29 @@ def native_rows(frame_height: int, world: int, rank: int) -> tuple[int, int]:
     return b.value, b.value + n.value
 
 
+def _native_halo(ksize: int, nitr) -> int:
+    """Halo rows of a native shard: r = ksize / 2, or nitr texture iterations deep."""
+    return ksize // 2 if nitr is None else nitr * texture_halo_rows(ksize)
+
+
 class NativeShard:
-    """This rank's shard of a row-sharded frame (one process per GPU, RCCL transport)."""
+    """This rank's shard of a row-sharded frame (one process per GPU, RCCL transport).
+    nitr given: the bilateral texture filter (vip_shard_create_texture; ksize is its k)."""
 
     def __init__(self, width: int, frame_height: int, ksize: int, rank: int, world: int, unique_id: bytes,
                  sigma_space: float = 10.0, sigma_color: float = 30.0, adaptive: bool = False, numerics: int = 0,
-                 timeout_ms: int = 180000):
+                 timeout_ms: int = 180000, nitr=None):
         import ctypes
         from . import _shard_lib as S
         self._h = ctypes.c_void_p()
         idb = ctypes.create_string_buffer(bytes(unique_id), S.VIP_SHARD_ID_BYTES)
-        S.call("vip_shard_create", ctypes.byref(self._h), _shard_kind(adaptive), width, frame_height, ksize,
-               sigma_space, sigma_color, numerics, world, rank, idb, int(timeout_ms))
-        self.geo = SlabGeometry(width, frame_height, ksize // 2, rank, world)
+        if nitr is None:
+            S.call("vip_shard_create", ctypes.byref(self._h), _shard_kind(adaptive), width, frame_height, ksize,
+                   sigma_space, sigma_color, numerics, world, rank, idb, int(timeout_ms))
+        else:
+            S.call("vip_shard_create_texture", ctypes.byref(self._h), width, frame_height, ksize, nitr, numerics,
+                   world, rank, idb, int(timeout_ms))
+        self.geo = SlabGeometry(width, frame_height, _native_halo(ksize, nitr), rank, world)
 
     def set_split(self, split: bool) -> None:
         """vip_shard_set_split: interior rows during the exchange, then the edge bands
@@ -379,15 +389,19 @@ class ShardGroup:
 
     def __init__(self, n: int, width: int, frame_height: int, ksize: int, transport: int = 1, devices=None,
                  sigma_space: float = 10.0, sigma_color: float = 30.0, adaptive: bool = False, numerics: int = 0,
-                 timeout_ms: int = 180000):
+                 timeout_ms: int = 180000, nitr=None):
         import ctypes
         from . import _shard_lib as S
         self.n = n
         self._hs = (ctypes.c_void_p * n)()
         devs = None if devices is None else (ctypes.c_int * n)(*devices)
-        S.call("vip_shard_create_group", self._hs, n, transport, devs, _shard_kind(adaptive), width, frame_height,
-               ksize, sigma_space, sigma_color, numerics, int(timeout_ms))
-        self.geos = [SlabGeometry(width, frame_height, ksize // 2, i, n) for i in range(n)]
+        if nitr is None:
+            S.call("vip_shard_create_group", self._hs, n, transport, devs, _shard_kind(adaptive), width, frame_height,
+                   ksize, sigma_space, sigma_color, numerics, int(timeout_ms))
+        else:
+            S.call("vip_shard_create_group_texture", self._hs, n, transport, devs, width, frame_height, ksize, nitr,
+                   numerics, int(timeout_ms))
+        self.geos = [SlabGeometry(width, frame_height, _native_halo(ksize, nitr), i, n) for i in range(n)]
 
     def set_split(self, split: bool) -> None:
         from . import _shard_lib as S
