@@ -499,7 +499,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
                 launch(sp[i % NBUF], dp[i % NBUF], sraw[h])
     res["exchange"] = (None if not multi else
-                       "native vip_shard (RCCL ncclSend/ncclRecv, overlapped with the interior rows)" if native else
+                       "native vip_shard (RCCL ncclSend/ncclRecv with the row neighbours)" if native else
                        f"torch.distributed P2P ({state.get('backend', args.backend)}), serial before the kernel")
 
     # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time per frame
@@ -583,6 +583,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             trial[split] = float(dt[0])
         best = min(trial, key=trial.get)
         sb.set_split(best)
+        res["exchange"] += ("; interior rows overlapped with the exchange, then the edge bands" if best
+                            else "; one launch over the own rows after the exchange")
         res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best
                             else "one launch after the exchange",
                             trial_ms_per_step={"split": round(trial[True], 4), "one_launch": round(trial[False], 4)})
@@ -766,8 +768,9 @@ def main():
             roof["valu_issue"] = valu_issue(args.config, kname, launch_ms)
         else:
             roof["avg_launch_note"] = ("per-rank device time of one step on one stream: "
-                                       + ("vip_shard_run (exchange overlapped with the interior rows, then the edges)"
-                                          if m["native"] else "the kernel after the serial exchange"))
+                                       + ("vip_shard_run (exchange, then the own rows: "
+                                          + m["split"]["chosen"] + ")" if m["native"]
+                                          else "the kernel after the serial exchange"))
 
     parts = m["parts"] or {}
     out = {
