@@ -68,8 +68,10 @@ typedef struct vip_shard_s* vip_shard_t;
  * rows plus (nitr - 1 - t) * vip_texture_halo_rows(ksize) rows on each side (a ghost zone
  * that shrinks to the own rows), so the result equals one single-GPU vip_texture_run of
  * the whole frame, bit for bit, with one exchange instead of nitr. The shard holds two
- * extra slabs for the iterations. No interior/edge split (every iteration reads the halo
- * region): vip_shard_set_split(h, 1) returns VIP_ERR_INVALID_ARGUMENT. */
+ * extra slabs for the iterations, so runs on one texture shard must not overlap (frames in
+ * flight on several streams take one shard each, as vip_texture handles do). No
+ * interior/edge split (every iteration reads the halo region): vip_shard_set_split(h, 1)
+ * returns VIP_ERR_INVALID_ARGUMENT. */
 
 /* Balanced contiguous row split: rank's first row and row count (no device call). */
 int vip_shard_rows(int frame_height, int nranks, int rank, int* row_begin, int* own_rows);
