@@ -169,15 +169,18 @@ def host_cores() -> tuple[int, str]:
     return n, model
 
 
+CPU_SECONDS = 10.0  # CPU work per baseline: at least 10 runs, about this many seconds
+
+
 def cpu_baseline(cfg) -> dict:
     """include/cpp numerics (oracle CPP profile) on the host cores, row bands in
     parallel threads, on a bounded sample of the same workload: one discarded warm-up,
-    then the mean of 10 runs (sample/benchmark/main.cpp:20-33, config.toml
-    execute_times = 10). Test infrastructure, reported beside the GPU number."""
+    then the mean of at least 10 runs (sample/benchmark/main.cpp:20-33, config.toml
+    execute_times = 10), as many as fill about CPU_SECONDS. Test infrastructure,
+    reported beside the GPU number."""
     from oracle import oracle as o
     threads, model = host_cores()
     w, k = cfg["width"], cfg["ksize"]
-    runs = 10
     if cfg.get("cpu_input") == "lenna":
         img = np.load(os.path.join(ROOT, "tests", "golden", "lenna_bgr.npz"))["bgr"]
         rows = img.shape[0]
@@ -200,10 +203,11 @@ def cpu_baseline(cfg) -> dict:
         fn = lambda: f(img, k, profile=o.CPP, threads=threads)  # noqa: E731
     fn()  # warm-up, discarded
     ts = []
-    for _ in range(runs):
+    while len(ts) < 10 or (sum(ts) < CPU_SECONDS and len(ts) < 2000):
         t0 = time.perf_counter()
         fn()
         ts.append(time.perf_counter() - t0)
+    runs = len(ts)
     dt = sum(ts) / runs
     return dict(value=round(rows * w / dt / 1e6, 4), unit="Mpixels/s", cores=threads, cpu_model=model, runs=runs,
                 warmup=1, ms_per_run=round(dt * 1e3, 2), kind="port",
