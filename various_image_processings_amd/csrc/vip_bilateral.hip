@@ -220,6 +220,13 @@ constexpr int lut_copies() {
 template <int R, int PLANES>
 constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : (R > 8 ? VIP_BIL_BIG_MAXW : 16); }
 
+#ifndef VIP_JBF_WIDE  // joint kernel on wide tiles with the 32-copy LUT (measurement knob)
+#define VIP_JBF_WIDE 0
+#endif
+#ifndef VIP_JBF_WIDE_MAX_R
+#define VIP_JBF_WIDE_MAX_R 8
+#endif
+
 #ifndef VIP_JBF_SHORT_LUT  // joint kernel: 32-entry clamped LUT when the colour LUT allows it
 #define VIP_JBF_SHORT_LUT 0
 #endif
@@ -281,6 +288,12 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
+#if VIP_JBF_WIDE
+    // joint filter on wide tiles (P = 4, one 256-pixel row per wave): two planes of
+    // 16 + 2R rows leave room for the 32-copy (bank-conflict free) LUT at 16 waves
+    if constexpr (JOINT && !FOLD && NE == 768 && R <= VIP_JBF_WIDE_MAX_R)
+        return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
+#endif
     if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
         const Tiling t = small_frame_tiling(a.width, a.out_rows);
         if (t.wide) {
@@ -300,7 +313,9 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     constexpr int P = WIDE ? 4 : outputs_per_thread<R, PLANES>();
     constexpr int TPR = WIDE ? 64 : 16;  // threads per tile row
     using G = Geom<R, P, TPR>;
-    constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
+    constexpr int COPIES = NE < 768 || (WIDE && pick_waves<R, PLANES, WAVES, 768 * 32, P, TPR>() == WAVES)
+                               ? 32
+                               : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int TH = WAVES * G::RPW;
     constexpr int LDS = lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
