@@ -56,7 +56,13 @@ def circle_taps(r: int) -> int:
 CONFIGS = {
     # C1 is the include/cpp (CPU) plumbing case: cpu_baseline times it; the GPU line is
     # the same filter on the same image through the HIP path
+    # c1: a 512x512 frame fills a quarter of the chip with 16-wave 256-pixel tiles (64
+    # workgroups), so 4 frames in flight on 4 streams run side by side (throughput tiling,
+    # set through vip_bilateral_set_waves/_wide; the library's default tiling minimises the
+    # latency of one frame instead: 256 4-wave tiles, 10.7 against 14.5 us per launch)
     "c1": dict(kind="bilateral", width=512, frame_height=512, ksize=11, data="lenna", cpu_input="lenna",
+               streams=4, tiling=(16, 2), kernel="void vip::bilateral_kernel<5, 16,",
+               kernel_label="bilateral_kernel<R=5> (16 waves x 256-px tiles, 64 per frame)",
                workload="bilateral r=5 sigma_s=10 sigma_r=30 lenna 512x512"),
     "c2": dict(kind="bilateral", width=3840, rows_per_rank=2160, ksize=15, workload="bilateral r=7 3840x2160 RGB8"),
     "c3": dict(kind="adaptive", width=3840, rows_per_rank=2160, ksize=15,
@@ -68,7 +74,7 @@ CONFIGS = {
     # not a BASELINE config: the largest ksize the reference runs (its shared memory
     # fits CUDA's 48 KB default up to 65), on the runtime-radius kernel
     "k65": dict(kind="bilateral", width=3840, rows_per_rank=2160, ksize=65,
-                kernel="void vip::stencil_rt_kernel<32, false, true, false>",
+                kernel="void vip::stencil_rt_kernel<32, false, true, false>", kernel_label="stencil_rt_kernel (R=32)",
                 workload="bilateral r=32 (ksize 65, the largest the reference runs) 3840x2160 RGB8"),
 }
 # algorithmic FP32 operations per in-support tap: bilateral
@@ -78,7 +84,7 @@ CONFIGS = {
 FLOP_PER_TAP = {"bilateral": 8, "adaptive": 13}
 
 
-DEFAULT_STEPS = {"c1": 2000, "c2": 2000, "c3": 1000, "c4": 500, "c5": 20, "k65": 100}
+DEFAULT_STEPS = {"c1": 6000, "c2": 2000, "c3": 1000, "c4": 500, "c5": 20, "k65": 100}
 
 
 def parse():
@@ -112,7 +118,8 @@ def parse():
     # the next frame's start. Measured (scripts/stream_bench.py, steady clocks): C2
     # 0.178 -> 0.173 ms, C3 0.327 -> 0.323, C4 0.717 -> 0.641 ms per frame with 2; 3 no
     # better. S must divide the 12 rotating buffers (a buffer always meets the same stream)
-    p.add_argument("--streams", type=int, default=2, choices=[1, 2, 3, 4, 6])
+    p.add_argument("--streams", type=int, default=None, choices=[1, 2, 3, 4, 6],
+                   help="default: the config's own (c1 4), else 2")
     # N>1: "strong" splits the metric's frame (C2/C3: 3840x2160) over the ranks (default
     # for c2, c3, c5), "weak" gives every rank a 2160-row slab of an (N*2160)-row frame
     # (default for c4). A strong c2/c3 line also carries the weak figure ("weak" key)
@@ -520,6 +527,9 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         # (S divides NBUF), so a halo receive into it is ordered after its last reader
         h = 0 if sample else i % S
         s = streams[h]
+        if not multi and not sample:  # one GPU: the launch names its stream; no torch stream context
+            run(i, s, h)
+            return
         if native:
             if sample:
                 m = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
@@ -716,7 +726,10 @@ def main():
 
     import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
 
-    S = args.streams
+    S = args.streams = args.streams or cfg.get("streams", 2)
+    if "tiling" in cfg and world == 1:  # the config's tile shape (include/vip.h tuning knobs)
+        vip.set_bilateral_waves(cfg["tiling"][0])
+        vip.set_bilateral_wide(cfg["tiling"][1])
     # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench)
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
     if args.scaling is None:
@@ -762,7 +775,7 @@ def main():
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
-                    kernel=f"{cfg['kind']}_kernel<R={r}>" if "kernel" not in cfg else f"stencil_rt_kernel (R={r})",
+                    kernel=cfg.get("kernel_label", f"{cfg['kind']}_kernel<R={r}>"),
                     avg_launch_ms=round(launch_ms, 4),
                     flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
                     gtaps_per_s=round(taps * px_per_rank / (launch_ms * 1e-3) / 1e9, 1),
@@ -770,6 +783,10 @@ def main():
                              bytes_per_px=6))
         if world == 1:  # the committed PMC summaries are whole-frame launches
             roof["valu_issue"] = valu_issue(args.config, kname, launch_ms)
+            if len(streams) > 1:  # the chip's rate with S frames in flight (launches overlap)
+                fl = flops / (ms_per_step * 1e-3) / 1e12
+                roof["in_flight"] = dict(achieved=round(fl, 3), frac=round(fl / PEAK_FP32_TFLOPS, 4), unit="TFLOP/s",
+                                         note=f"{len(streams)} frames in flight: flops per frame / ms_per_step")
         else:
             roof["avg_launch_note"] = ("per-rank device time of one step on one stream: "
                                        + ("vip_shard_run (exchange, then the own rows: "
@@ -793,6 +810,7 @@ def main():
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows, "data": args.data,
                    "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
+                   **({"tiling": cfg["kernel_label"]} if "tiling" in cfg and world == 1 else {}),
                    **({"texture_mode": args.texture_mode} if cfg["kind"] == "texture" and world == 1 else {}),
                    **({"backend": state.get("backend"), "exchange": m["exchange"]} if state["multi"] else {}),
                    **({"exchange_fallback": m["exchange_fallback"]} if m.get("exchange_fallback") else {})},

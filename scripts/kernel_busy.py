@@ -21,13 +21,14 @@ def main():
     # (sorted by start: a launch overlaps an earlier one iff it starts before their
     # latest end, a later one iff it ends after the next start). Back-to-back launches on
     # one stream can touch by a few hundred ns in the trace (the next start is stamped
-    # before the previous end is), so an overlap below TOL_NS does not count.
-    TOL_NS = 2000
+    # before the previous end is; measured <= 156 ns), so an overlap below 1 us and below
+    # a tenth of the launch does not count.
     iso = []
     end_max = -1
     for i, (s, e, _) in enumerate(iv):
         nxt = iv[i + 1][0] if i + 1 < len(iv) else e
-        iso.append(s >= end_max - TOL_NS and e <= nxt + TOL_NS)
+        tol = min(1000, (e - s) // 10)
+        iso.append(s >= end_max - tol and e <= nxt + tol)
         end_max = max(end_max, e)
     busy, cur_s, cur_e = 0, None, None
     for s, e, _ in iv:
