@@ -74,7 +74,8 @@ struct FoldRank {  // table index of tap (|ky|, |kx|)
 #else
 #define VIP_BIL_WPE_ATTR
 #endif
-template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false, int TPR = 16>
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false, int TPR = 16,
+          bool SAT = false>
 __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(const StencilArgs a) {
     using G = Geom<R, P, TPR>;
     constexpr int NT = WAVES * 64;
@@ -86,7 +87,9 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     uint32_t* const lut = lds;
     constexpr int NTAB = FOLD ? disc_r2_count(R) : 1;
     static_assert(!FOLD || (NE == 32 && COPIES == 32), "folded tables: 32 entries x 32 copies");
-    uint32_t* const gplane = lds + NTAB * NE * COPIES;
+    static_assert(!SAT || FOLD, "the saturating address serves the folded tables");
+    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE>;  // SAT: tables from byte SL::T, planes at SL::PL
+    uint32_t* const gplane = SAT ? lds + SL::PL / 4 : lds + NTAB * NE * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
     const int tid = threadIdx.x;
@@ -95,13 +98,15 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     const int tx = lane % TPR;
     const int ty = wave * G::RPW + lane / TPR;
     const uint32_t lane4 = (uint32_t)(lane & (COPIES - 1)) << 2;  // this lane's LUT copy
+    const uint32_t sbias = (uint32_t)SL::B0 + lane4;                // SAT: register bias of the address
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     VIP_RT_STAMP(0);
     // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
     int tile = blockIdx.x;
     TilePrefetch<R, ROWS, NT, P, TPR> pg, ps;
-    LutStage<NT, NTAB * NE, COPIES> ls;  // once per workgroup; its reads go out first
+    // once per workgroup; its reads go out first
+    std::conditional_t<SAT, SatStage<NT, SL>, LutStage<NT, NTAB * NE, COPIES>> ls;
     ls.load(FOLD ? a.fold : a.color);
     {
         const int mt = xcd_tile(tile, a.tiles_total);
@@ -109,7 +114,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
         pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
-    ls.store(lut);
+    ls.store(SAT ? lds + SL::T / 4 : lut);
     pg.commit(gplane);
     if constexpr (JOINT) ps.commit(splane);
     __syncthreads();
@@ -153,6 +158,11 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
                     // colour weight address: v_sad_u8 (|db|+|dg|+|dr|) -> word d*COPIES + lane copy
                     auto widx = [&](uint32_t g, f2, f2, int i, int kx) {
                         uint32_t d = __builtin_amdgcn_sad_u8(g, ctr[i], 0u);
+                        if constexpr (SAT) {  // min(d*S + bias, 65535) + table offset (immediate)
+                            constexpr FoldRank<R> rank;
+                            return sat_addr(d, SL::S, sbias) +
+                                   (uint32_t)(SL::T - SL::B0 + 128 * rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)]);
+                        }
                         if constexpr (NE < 768) d = d < NE - 1 ? d : NE - 1;
                         const uint32_t ad = (d << (COPIES == 32 ? 7 : 6)) | lane4;
                         if constexpr (FOLD) {
@@ -162,7 +172,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
                         return ad;
                     };
                     row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT, decltype(widx)&, FOLD,
-                             JOINT ? VIP_PIPE_DEPTH : VIP_BIL_PIPE_DEPTH>(
+                             JOINT ? VIP_PIPE_DEPTH : VIP_BIL_PIPE_DEPTH, SAT>(
                         gplane, splane, row_off, wsv, lut_bytes, widx, a01, a2k);
                     if constexpr (ROW_UNROLL) fence_accumulators(a01, a2k);
             });
@@ -277,37 +287,55 @@ inline Tiling small_frame_tiling(int width, int out_rows) {
     return best;
 }
 
-template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE = false>
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE = false, bool SAT = false>
 static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream);
 
-template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false>
+// LDS of a SAT launch (planes, then the saturating-address tables)
+template <int R, int WAVES, int PLANES, int P>
+constexpr int sat_lds_bytes() {
+    return SatLut<R, 4 * PLANES * (WAVES * Geom<R, P>::RPW + 2 * R) * Geom<R, P>::S>::BYTES;
+}
+template <int R, int PLANES, int MAXW, int P>
+constexpr int pick_waves_sat() {
+    if (MAXW >= 16 && sat_lds_bytes<R, 16, PLANES, P>() <= kLdsBudget) return 16;
+    if (MAXW >= 12 && sat_lds_bytes<R, 12, PLANES, P>() <= kLdsBudget) return 12;
+    if (MAXW >= 8 && sat_lds_bytes<R, 8, PLANES, P>() <= kLdsBudget) return 8;
+    return sat_lds_bytes<R, 4, PLANES, P>() <= kLdsBudget ? 4 : 0;
+}
+
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false, bool SAT = false>
 static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
     constexpr int P = outputs_per_thread<R, PLANES>();
     constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
-    constexpr int WAVES = pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
+    constexpr int WAVES = SAT ? pick_waves_sat<R, PLANES, max_waves<R, PLANES>(), P>()
+                              : pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
+    if constexpr (SAT) {
+        return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, WAVES, false, true>(a, stream);
+    } else {
 #if VIP_JBF_WIDE
-    // joint filter on wide tiles (P = 4, one 256-pixel row per wave): two planes of
-    // 16 + 2R rows leave room for the 32-copy (bank-conflict free) LUT at 16 waves
-    if constexpr (JOINT && !FOLD && NE == 768 && R <= VIP_JBF_WIDE_MAX_R)
-        return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
+        // joint filter on wide tiles (P = 4, one 256-pixel row per wave): two planes of
+        // 16 + 2R rows leave room for the 32-copy (bank-conflict free) LUT at 16 waves
+        if constexpr (JOINT && !FOLD && NE == 768 && R <= VIP_JBF_WIDE_MAX_R)
+            return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
 #endif
-    if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
-        const Tiling t = small_frame_tiling(a.width, a.out_rows);
-        if (t.wide) {
-            if (t.waves == 16) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
-            if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8, true>(a, stream);
-            return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4, true>(a, stream);
+        if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
+            const Tiling t = small_frame_tiling(a.width, a.out_rows);
+            if (t.wide) {
+                if (t.waves == 16) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
+                if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8, true>(a, stream);
+                return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4, true>(a, stream);
+            }
+            if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8>(a, stream);
+            if (t.waves == 4) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4>(a, stream);
         }
-        if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8>(a, stream);
-        if (t.waves == 4) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 4>(a, stream);
+        return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, WAVES>(a, stream);
     }
-    return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, WAVES>(a, stream);
 }
 
-template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE>
+template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE, bool SAT>
 static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
     constexpr int P = WIDE ? 4 : outputs_per_thread<R, PLANES>();
@@ -318,9 +346,10 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
                                : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int TH = WAVES * G::RPW;
-    constexpr int LDS = lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
+    constexpr int LDS = SAT ? sat_lds_bytes<R, WAVES, PLANES, P>() : lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
     static_assert(LDS <= kLdsBudget, "tile does not fit LDS");
-    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR>;
+    static_assert(!SAT || TPR == 16, "SAT: 128-pixel tiles");
+    auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
@@ -334,6 +363,8 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
 
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
+    if constexpr (JOINT && R <= kSatMaxR)  // saturating-address folded tables (SatLut)
+        if (a.fold && a.lut_nonzero <= SatLut<R, 0>::DZ) return launch_bilateral_ne<R, JOINT, FMA, 32, true, true>(a, stream);
     if constexpr (JOINT && R <= kFoldMaxR)
         if (a.fold) return launch_bilateral_ne<R, JOINT, FMA, 32, true>(a, stream);
     if constexpr (JOINT && VIP_JBF_SHORT_LUT)

@@ -331,7 +331,7 @@ static int upload_fold(vip_bilateral_s* h, float sigma_color) {
     const int R = h->radius;
     float wc[768];
     build_color(768, sigma_color, h->numerics, wc);
-    float fold[(kFoldMaxR * kFoldMaxR + 1) * 32];
+    float fold[(kFoldTablesMaxR * kFoldTablesMaxR + 1) * 32];
     int ntab = 0;
     for (int v = 0; v <= R * R; ++v) {
         if (!is_disc_r2(R, v)) continue;
@@ -361,7 +361,7 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
     int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics, &h->lut_nonzero);
     if (!rc) rc = upload_rt_tables(h->radius, sigma_space, h->numerics, &h->rt);
-    if (!rc && h->lut_nonzero <= 31 && h->radius <= kFoldMaxR) rc = upload_fold(h, sigma_color);
+    if (!rc && h->lut_nonzero <= 31 && h->radius <= kFoldTablesMaxR) rc = upload_fold(h, sigma_color);
     if (rc) {
         vip_bilateral_destroy(h);
         return rc;

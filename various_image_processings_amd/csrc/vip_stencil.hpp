@@ -13,6 +13,7 @@
 // 8*(l%16) .. 8*(l%16)+7 (P = 8 horizontally adjacent outputs per thread).
 #pragma once
 
+#include <type_traits>
 #include <utility>
 
 #include "vip_common.hpp"
@@ -28,6 +29,36 @@ constexpr int kLdsBudget = 160 * 1024;
 #define VIP_JBF_FOLD_MAX_R 0
 #endif
 constexpr int kFoldMaxR = VIP_JBF_FOLD_MAX_R;
+#ifndef VIP_JBF_SAT_MAX_R  // joint kernel: folded tables behind a saturating address (SatLut) up to this radius
+#define VIP_JBF_SAT_MAX_R 6
+#endif
+constexpr int kSatMaxR = VIP_JBF_SAT_MAX_R;
+constexpr int kFoldTablesMaxR = kFoldMaxR > kSatMaxR ? kFoldMaxR : kSatMaxR;  // handles upload the tables
+
+// Folded joint-bilateral LUT behind a saturating address (SAT). One table per distinct
+// squared tap distance r^2 (NTAB of them) holds RN(ws(r^2) * wc[d]), 32 interleaved
+// copies each; the tables of one distance d sit side by side, S = NTAB * 128 bytes per d,
+// from LDS byte T on: entry (d, table k, copy c) at T + d*S + 128k + 4c. A tap's address
+// is one v_mad_legacy_u16 with the clamp bit, min(d*S + B0 + 4c, 65535), plus the
+// compile-time T - B0 + 128k in the ds_read immediate. Up to d = DZ that is the entry
+// itself; every larger d saturates to 65535, which B0 = 65535 - DZ*S - 124 places on entry
+// (DZ, k, 31) -- an exact zero whenever the colour LUT is zero from DZ on (the texture
+// filter's sigma_color sqrt(3): zero from d = 25). So the clamp costs no instruction and
+// the spatial multiply is folded away: per tap v_sad_u8, v_mad_legacy_u16, ds_read,
+// 3 v_fma, v_add (the 32-copy reads stay bank-conflict free; lanes that saturate read one
+// broadcast word). T = B0 rounded up to 16 keeps the immediate small and >= 0; the tile
+// planes (PB bytes) go below the tables when they fit under B0, else after them.
+template <int R, int PB>
+struct SatLut {
+    static constexpr int NTAB = disc_r2_count(R);
+    static constexpr int S = NTAB * 128;
+    static constexpr int DZ = (65535 - 124) / S < 31 ? (65535 - 124) / S : 31;  // fold tables hold d < 32
+    static constexpr int B0 = 65535 - DZ * S - 124;
+    static constexpr int T = round_up(B0, 16);
+    static constexpr int PL = PB <= B0 ? 0 : round_up(T + (DZ + 1) * S, 16);  // plane offset
+    static constexpr int BYTES = PB <= B0 ? T + (DZ + 1) * S : PL + PB;
+    static_assert(DZ >= 0 && T - B0 + (NTAB - 1) * 128 <= 65535, "ds_read immediate range");
+};
 
 struct StencilArgs {
     const uint8_t* src;
@@ -310,6 +341,44 @@ struct LutStage {
     }
 };
 
+// SatLut staging: the fold tables ([NTAB][32] in device memory, d < 32) into the
+// [d][table][copy] layout, d = 0..DZ, at LDS byte T (the store() argument points there).
+template <int NT, class SL>
+struct SatStage {
+    static constexpr int WPD = SL::NTAB * 32;           // words per distance
+    static constexpr int N = (SL::DZ + 1) * WPD / 4;    // uint4 stores
+    static constexpr int K = (N + NT - 1) / NT;
+    uint32_t v[K];
+
+    __device__ __forceinline__ void load(const float* fold) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int q = (int)threadIdx.x + k * NT;
+            const int w = 4 * q, d = w / WPD, t = (w - d * WPD) >> 5;
+            if (N % NT == 0 || q < N) v[k] = __float_as_uint(fold[t * 32 + d]);
+        }
+    }
+    __device__ __forceinline__ void store(uint32_t* lut) const {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int q = (int)threadIdx.x + k * NT;
+            if (N % NT == 0 || q < N) *reinterpret_cast<uint4*>(lut + 4 * q) = make_uint4(v[k], v[k], v[k], v[k]);
+        }
+    }
+};
+
+// min(d * s + bias, 65535) in one VALU op (the clamp bit saturates the u16 result);
+// the legacy encoding zeroes the destination's high half (checked on gfx950 by
+// microbench/sat_addr.hip, which also measures its issue rate in the tap mix).
+#ifndef VIP_SAT_INSN
+#define VIP_SAT_INSN "v_mad_legacy_u16"
+#endif
+__device__ __forceinline__ uint32_t sat_addr(uint32_t d, uint32_t s, uint32_t bias) {
+    uint32_t r;
+    __asm__(VIP_SAT_INSN " %0, %1, %2, %3 clamp" : "=v"(r) : "v"(d), "s"(s), "v"(bias));
+    return r;
+}
+
 template <int NT, int ENTRIES, int COPIES>
 __device__ __forceinline__ void stage_lut(uint32_t* lut, const float* color) {
     LutStage<NT, ENTRIES, COPIES> s;
@@ -402,8 +471,11 @@ __device__ __forceinline__ void fence_accumulators(f2 (&a01)[P], f2 (&a2k)[P]) {
 #ifndef VIP_ROW_LOOKAHEAD
 #define VIP_ROW_LOOKAHEAD 4  // columns between a chunk's LDS read and its first use
 #endif
+// ABS: widx returns an absolute LDS byte address (the kernel's dynamic LDS starts at 0),
+// read through an address-space-3 pointer, so a constant part of it lands in the ds_read
+// immediate instead of a v_add of the LDS base.
 template <int HW, int L, int C0, int NC, bool FMA, bool PK, int P, bool TWO, class WIdx, bool FOLD = false,
-          int D = VIP_PIPE_DEPTH>
+          int D = VIP_PIPE_DEPTH, bool ABS = false>
 __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t* splane, int row_off,
                                          const float (&wsv)[HW + 1], const char* lut, WIdx&& widx,
                                          f2 (&a01)[P], f2 (&a2k)[P]) {
@@ -436,7 +508,11 @@ __device__ __forceinline__ void row_taps(const uint32_t* gplane, const uint32_t*
         for (int i = 0; i < P; ++i) {
             const int kx = j - L - i;
             if (kx < -HW || kx > HW) continue;
-            wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b], n21[b], i, kx));
+            if constexpr (ABS)
+                wc[b][i] = *reinterpret_cast<const __attribute__((address_space(3))) float*>(
+                    (size_t)widx(g, n01[b], n21[b], i, kx));
+            else
+                wc[b][i] = *reinterpret_cast<const float*>(lut + widx(g, n01[b], n21[b], i, kx));
         }
     };
 #pragma unroll
