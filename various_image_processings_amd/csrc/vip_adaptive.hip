@@ -34,8 +34,18 @@ constexpr bool adaptive_vbox() {
 // NE: LUT entries in LDS (1536 x 16 copies; or 512 x 32 copies, bank-conflict free, when
 // the colour LUT is exactly zero from entry 511 on -- sigma_color 30 underflows past
 // d = 431 -- with the index clamped to 511: one v_min_u32 per tap).
-template <int R, int WAVES, bool FMA, int P, int NE = 1536>
+// SAT (NE = 512, 32 copies): the index clamp costs no instruction -- the LUT address is
+// one v_mad_legacy_u16 with the clamp bit, min(d*128 + B0 + 4c, 65535), in place of the
+// v_lshl_or, and every d > 511 saturates onto entry (511, copy 31), an exact zero (the
+// SatLut scheme of vip_stencil.hpp with one table). The table sits at LDS byte 16.
+constexpr int kAdaSatB0 = 65535 - 511 * 128 - 124;  // 3
+constexpr int kAdaSatT = 16;                         // round_up(kAdaSatB0, 16): table byte offset
+template <int NE, bool SAT>
+constexpr int ada_lut_words() { return NE * (NE < 1536 ? 32 : 16) + (SAT ? kAdaSatT / 4 : 0); }
+
+template <int R, int WAVES, bool FMA, int P, int NE = 1536, bool SAT = false>
 __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs a) {
+    static_assert(!SAT || NE == 512, "SAT: 512 entries x 32 copies");
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
     constexpr int TH = WAVES * 4;
@@ -50,14 +60,14 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     // the plane rows' unused tail words), then each thread slides its K-column windows
     // over them. Fits the LDS for R <= 8; larger radii keep the per-thread square sums.
     constexpr int VW = G::GROUPS * 4;          // plane words in use per row (TW + 2L)
-    constexpr bool VBOX = adaptive_vbox<R, P, WAVES, NE * (NE < 1536 ? 32 : 16)>();
+    constexpr bool VBOX = adaptive_vbox<R, P, WAVES, ada_lut_words<NE, SAT>()>();
     // straight-line rows where the separable box sums apply (R <= 8); the larger
     // radii keep the row loop (code size and build time)
     constexpr bool ROW_UNROLL = VIP_ADA_UNROLL != 0 && VBOX;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* const lut = lds;
+    uint32_t* const lut = lds + (SAT ? kAdaSatT / 4 : 0);
     constexpr int COPIES = NE < 1536 ? 32 : 16;
-    uint32_t* const plane = lds + NE * COPIES;
+    uint32_t* const plane = lds + ada_lut_words<NE, SAT>();
     uint32_t* const vrb = plane + ROWS * G::S;  // VBOX: TH x VW words
 
     const int tid = threadIdx.x;
@@ -66,6 +76,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     const int tx = lane & 15;
     const int ty = wave * 4 + (lane >> 4);
     const uint32_t lane16 = (uint32_t)(lane & (COPIES - 1)) << 2;
+    const uint32_t sbias = (uint32_t)kAdaSatB0 + lane16;  // SAT: register bias of the address
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x
@@ -264,11 +275,12 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
                         const float d2 = (n21.x - c2f[i]) - o2[i];
                         const float dist = (__builtin_fabsf(d0) + __builtin_fabsf(d1)) + __builtin_fabsf(d2);
                         uint32_t d = (uint32_t)dist;
+                        if constexpr (SAT) return sat_addr(d, 128u, sbias) + (uint32_t)(kAdaSatT - kAdaSatB0);
                         if constexpr (NE < 1536) d = d < NE - 1 ? d : NE - 1;
                         return (d << (COPIES == 32 ? 7 : 6)) | lane16;
                     };
-                    row_taps<HW, G::L, C0, NC, FMA, false, P, false>(plane, plane, row_off, wsv, lut_bytes, widx, a01,
-                                                                     a2k);
+                    row_taps<HW, G::L, C0, NC, FMA, false, P, false, decltype(widx)&, false, VIP_PIPE_DEPTH, SAT>(
+                        plane, plane, row_off, wsv, lut_bytes, widx, a01, a2k);
                     if constexpr (ROW_UNROLL) fence_accumulators(a01, a2k);
             });
 
@@ -287,21 +299,24 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
 #ifndef VIP_ADA_SHORT_LUT
 #define VIP_ADA_SHORT_LUT 0
 #endif
+#ifndef VIP_ADA_SAT  // 512 x 32 conflict-free LUT behind the saturating address
+#define VIP_ADA_SAT 1
+#endif
 
-template <int R, bool FMA, int NE>
+template <int R, bool FMA, int NE, bool SAT = false>
 static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     // P = 8 outputs per thread needs ~170 VGPRs (per-output centre/offset floats,
     // accumulators, pipelined LUT reads) -> 8 waves; P = 4 fits 128 -> 16 waves
     constexpr int P = VIP_ADA_P;
     using G = Geom<R, P>;
-    constexpr int LUTW = NE * (NE < 1536 ? 32 : 16);
+    constexpr int LUTW = ada_lut_words<NE, SAT>();
     constexpr int WAVES = pick_waves<R, 1, P == 8 ? 8 : 16, LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     constexpr int TH = WAVES * 4;
     constexpr int LDS = lds_bytes<R, WAVES, 1, LUTW, P>() +
                         (adaptive_vbox<R, P, WAVES, LUTW>() ? 4 * TH * G::GROUPS * 4 : 0);
     static_assert(LDS <= kLdsBudget, "adaptive tile does not fit LDS");
-    auto kern = adaptive_kernel<R, WAVES, FMA, P, NE>;
+    auto kern = adaptive_kernel<R, WAVES, FMA, P, NE, SAT>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
     StencilArgs args = a;
@@ -315,6 +330,8 @@ static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
 
 template <int R, bool FMA>
 static int launch_adaptive_r(const StencilArgs& a, hipStream_t stream) {
+    if constexpr (VIP_ADA_SAT != 0)
+        if (a.lut_nonzero <= 511) return launch_adaptive_ne<R, FMA, 512, true>(a, stream);
     if constexpr (VIP_ADA_SHORT_LUT != 0)
         if (a.lut_nonzero <= 511) return launch_adaptive_ne<R, FMA, 512>(a, stream);
     return launch_adaptive_ne<R, FMA, 1536>(a, stream);
