@@ -87,8 +87,9 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     uint32_t* const lut = lds;
     constexpr int NTAB = FOLD ? disc_r2_count(R) : 1;
     static_assert(!FOLD || (NE == 32 && COPIES == 32), "folded tables: 32 entries x 32 copies");
-    static_assert(!SAT || FOLD, "the saturating address serves the folded tables");
-    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE>;  // SAT: tables from byte SL::T, planes at SL::PL
+    // SAT: tables from byte SL::T, planes at SL::PL (folded: one table per r^2, d <= 31;
+    // unfolded: the colour LUT, d <= 511, times the spatial weight per tap)
+    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE, FOLD ? disc_r2_count(R) : 1, FOLD ? 31 : 511>;
     uint32_t* const gplane = SAT ? lds + SL::PL / 4 : lds + NTAB * NE * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
@@ -159,9 +160,12 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
                     auto widx = [&](uint32_t g, f2, f2, int i, int kx) {
                         uint32_t d = __builtin_amdgcn_sad_u8(g, ctr[i], 0u);
                         if constexpr (SAT) {  // min(d*S + bias, 65535) + table offset (immediate)
-                            constexpr FoldRank<R> rank;
-                            return sat_addr(d, SL::S, sbias) +
-                                   (uint32_t)(SL::T - SL::B0 + 128 * rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)]);
+                            uint32_t off = (uint32_t)(SL::T - SL::B0);
+                            if constexpr (FOLD) {
+                                constexpr FoldRank<R> rank;
+                                off += 128u * rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)];
+                            }
+                            return sat_addr(d, SL::S, sbias) + off;
                         }
                         if constexpr (NE < 768) d = d < NE - 1 ? d : NE - 1;
                         const uint32_t ad = (d << (COPIES == 32 ? 7 : 6)) | lane4;
@@ -237,6 +241,13 @@ constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : (R > 8 ? VIP_BIL
 #define VIP_JBF_WIDE_MAX_R 8
 #endif
 
+// Plain kernel on the 512-entry saturating-address LUT (SatLut, 64 KiB, v_mad_legacy_u16
+// in place of the v_lshl_or) when the colour LUT allows it. Measured slower, so off: C2
+// 172.3 -> 175.4 us, the C5 slab 3198 -> 3296 us (profiles/r03_sat_variants.txt).
+#ifndef VIP_BIL_SAT
+#define VIP_BIL_SAT 0
+#endif
+
 #ifndef VIP_JBF_SHORT_LUT  // joint kernel: 32-entry clamped LUT when the colour LUT allows it
 #define VIP_JBF_SHORT_LUT 0
 #endif
@@ -290,17 +301,18 @@ inline Tiling small_frame_tiling(int width, int out_rows) {
 template <int R, bool JOINT, bool FMA, int NE, bool FOLD, int WAVES, bool WIDE = false, bool SAT = false>
 static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream);
 
-// LDS of a SAT launch (planes, then the saturating-address tables)
-template <int R, int WAVES, int PLANES, int P>
+// LDS of a SAT launch (the saturating-address tables and the planes)
+template <int R, int WAVES, int PLANES, int P, bool FOLD>
 constexpr int sat_lds_bytes() {
-    return SatLut<R, 4 * PLANES * (WAVES * Geom<R, P>::RPW + 2 * R) * Geom<R, P>::S>::BYTES;
+    return SatLut<R, 4 * PLANES * (WAVES * Geom<R, P>::RPW + 2 * R) * Geom<R, P>::S, FOLD ? disc_r2_count(R) : 1,
+                  FOLD ? 31 : 511>::BYTES;
 }
-template <int R, int PLANES, int MAXW, int P>
+template <int R, int PLANES, int MAXW, int P, bool FOLD>
 constexpr int pick_waves_sat() {
-    if (MAXW >= 16 && sat_lds_bytes<R, 16, PLANES, P>() <= kLdsBudget) return 16;
-    if (MAXW >= 12 && sat_lds_bytes<R, 12, PLANES, P>() <= kLdsBudget) return 12;
-    if (MAXW >= 8 && sat_lds_bytes<R, 8, PLANES, P>() <= kLdsBudget) return 8;
-    return sat_lds_bytes<R, 4, PLANES, P>() <= kLdsBudget ? 4 : 0;
+    if (MAXW >= 16 && sat_lds_bytes<R, 16, PLANES, P, FOLD>() <= kLdsBudget) return 16;
+    if (MAXW >= 12 && sat_lds_bytes<R, 12, PLANES, P, FOLD>() <= kLdsBudget) return 12;
+    if (MAXW >= 8 && sat_lds_bytes<R, 8, PLANES, P, FOLD>() <= kLdsBudget) return 8;
+    return sat_lds_bytes<R, 4, PLANES, P, FOLD>() <= kLdsBudget ? 4 : 0;
 }
 
 template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false, bool SAT = false>
@@ -309,7 +321,7 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int P = outputs_per_thread<R, PLANES>();
     constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
-    constexpr int WAVES = SAT ? pick_waves_sat<R, PLANES, max_waves<R, PLANES>(), P>()
+    constexpr int WAVES = SAT ? pick_waves_sat<R, PLANES, max_waves<R, PLANES>(), P, FOLD>()
                               : pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
     static_assert(WAVES > 0, "tile does not fit LDS");
     if constexpr (SAT) {
@@ -346,7 +358,7 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
                                : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int TH = WAVES * G::RPW;
-    constexpr int LDS = SAT ? sat_lds_bytes<R, WAVES, PLANES, P>() : lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
+    constexpr int LDS = SAT ? sat_lds_bytes<R, WAVES, PLANES, P, FOLD>() : lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
     static_assert(LDS <= kLdsBudget, "tile does not fit LDS");
     static_assert(!SAT || TPR == 16, "SAT: 128-pixel tiles");
     auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT>;
@@ -363,6 +375,12 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
 
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
+    if constexpr (!JOINT && VIP_BIL_SAT) {  // plain filter, 128-pixel 16-wave tiles: 512 x 32 LUT (SatLut)
+        if (a.lut_nonzero <= 511) {
+            const Tiling t = R <= VIP_BIL_SMALL_MAX_R ? small_frame_tiling(a.width, a.out_rows) : Tiling{16, false};
+            if (t.waves == 16 && !t.wide) return launch_bilateral_ne<R, JOINT, FMA, 768, false, true>(a, stream);
+        }
+    }
     if constexpr (JOINT && R <= kSatMaxR)  // saturating-address folded tables (SatLut)
         if (a.fold && a.lut_nonzero <= SatLut<R, 0>::DZ) return launch_bilateral_ne<R, JOINT, FMA, 32, true, true>(a, stream);
     if constexpr (JOINT && R <= kFoldMaxR)
@@ -378,7 +396,7 @@ static int launch_bilateral_dispatch(int radius, const StencilArgs& a, hipStream
 #define VIP_CASE(RR) \
     case RR: return launch_bilateral_r<RR, JOINT, FMA>(a, stream);
 #ifdef VIP_ONLY_R7
-        VIP_CASE(4) VIP_CASE(7)
+        VIP_CASE(4) VIP_CASE(7) VIP_CASE(15)
 #else
         VIP_CASE(1) VIP_CASE(2) VIP_CASE(3) VIP_CASE(4) VIP_CASE(5) VIP_CASE(6) VIP_CASE(7) VIP_CASE(8)
         VIP_CASE(9) VIP_CASE(10) VIP_CASE(11) VIP_CASE(12) VIP_CASE(13) VIP_CASE(14) VIP_CASE(15)

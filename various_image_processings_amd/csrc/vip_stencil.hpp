@@ -48,11 +48,14 @@ constexpr int kFoldTablesMaxR = kFoldMaxR > kSatMaxR ? kFoldMaxR : kSatMaxR;  //
 // 3 v_fma, v_add (the 32-copy reads stay bank-conflict free; lanes that saturate read one
 // broadcast word). T = B0 rounded up to 16 keeps the immediate small and >= 0; the tile
 // planes (PB bytes) go below the tables when they fit under B0, else after them.
-template <int R, int PB>
+// NTAB_ = 1, DZMAX = 511: the unfolded colour LUT of the plain filter (zero from d <= 511,
+// e.g. sigma_color 30: zero from 432) as 512 entries x 32 copies -- 64 KiB instead of 96,
+// the v_lshl_or of the address replaced by the (fast-class) v_mad_legacy_u16.
+template <int R, int PB, int NTAB_ = disc_r2_count(R), int DZMAX = 31>
 struct SatLut {
-    static constexpr int NTAB = disc_r2_count(R);
+    static constexpr int NTAB = NTAB_;
     static constexpr int S = NTAB * 128;
-    static constexpr int DZ = (65535 - 124) / S < 31 ? (65535 - 124) / S : 31;  // fold tables hold d < 32
+    static constexpr int DZ = (65535 - 124) / S < DZMAX ? (65535 - 124) / S : DZMAX;  // fold tables hold d < 32
     static constexpr int B0 = 65535 - DZ * S - 124;
     static constexpr int T = round_up(B0, 16);
     static constexpr int PL = PB <= B0 ? 0 : round_up(T + (DZ + 1) * S, 16);  // plane offset
