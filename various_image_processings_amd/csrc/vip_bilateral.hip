@@ -53,12 +53,12 @@ __device__ __forceinline__ void vip_rt_stamp(int k) {
 // handle's LUT is exactly zero from entry 31 on (small sigma_color: the texture
 // filter's JBF has sigma_color sqrt(3), nonzero up to d = 24): the distance is then
 // clamped to 31 (one v_min_u32 per tap) and the 32-copy table takes 4 KiB.
-// FOLD (with NE = 32): one such table per distinct squared tap distance r^2, holding
+// FOLD (with SAT, NE = 32): one table per distinct squared tap distance r^2, holding
 // the full weight RN(ws(r^2) * wc[d]) -- the same float product the unfolded taps
 // form, so bit-identical -- addressed by the tap's compile-time table offset (the
-// ds_read immediate): per tap v_sad_u8, v_min_u32, v_lshl_or, 3 v_fma, v_add and no
-// spatial v_mul; with 32 copies the reads are bank-conflict free. At R = 4 (the C4
-// JBF) 10 tables = 40 KiB, against 48 KiB for the 16-copy (2-way conflicting) LUT.
+// ds_read immediate) behind the saturating address (SatLut, vip_stencil.hpp): per tap
+// v_sad_u8, v_mad_legacy_u16, 3 v_fma, v_add and no spatial v_mul, bank-conflict free.
+// (Round 2 measured the folded tables behind a v_min clamp + v_lshl_or: 7 VALU, slower.)
 template <int R>
 struct FoldRank {  // table index of tap (|ky|, |kx|)
     int t[(R + 1) * (R + 1)];
@@ -86,10 +86,10 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
     constexpr int NTAB = FOLD ? disc_r2_count(R) : 1;
-    static_assert(!FOLD || (NE == 32 && COPIES == 32), "folded tables: 32 entries x 32 copies");
-    // SAT: tables from byte SL::T, planes at SL::PL (folded: one table per r^2, d <= 31;
+    static_assert(!FOLD || (SAT && NE == 32 && COPIES == 32), "folded tables: saturating address, 32 copies");
+    // SAT: tables from byte SL::T, planes at SL::PL (folded: one table per r^2, d <= DZ;
     // unfolded: the colour LUT, d <= 511, times the spatial weight per tap)
-    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE, FOLD ? disc_r2_count(R) : 1, FOLD ? 31 : 511>;
+    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE, FOLD ? disc_r2_count(R) : 1, FOLD ? kSatFoldDz : 511>;
     uint32_t* const gplane = SAT ? lds + SL::PL / 4 : lds + NTAB * NE * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
@@ -168,12 +168,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
                             return sat_addr(d, SL::S, sbias) + off;
                         }
                         if constexpr (NE < 768) d = d < NE - 1 ? d : NE - 1;
-                        const uint32_t ad = (d << (COPIES == 32 ? 7 : 6)) | lane4;
-                        if constexpr (FOLD) {
-                            constexpr FoldRank<R> rank;
-                            return ad + (uint32_t)rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)] * (NE * COPIES * 4);
-                        }
-                        return ad;
+                        return (d << (COPIES == 32 ? 7 : 6)) | lane4;
                     };
                     row_taps<HW, G::L, C0, NC, FMA, false, P, JOINT, decltype(widx)&, FOLD,
                              JOINT ? VIP_PIPE_DEPTH : VIP_BIL_PIPE_DEPTH, SAT>(
@@ -305,7 +300,7 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream);
 template <int R, int WAVES, int PLANES, int P, bool FOLD>
 constexpr int sat_lds_bytes() {
     return SatLut<R, 4 * PLANES * (WAVES * Geom<R, P>::RPW + 2 * R) * Geom<R, P>::S, FOLD ? disc_r2_count(R) : 1,
-                  FOLD ? 31 : 511>::BYTES;
+                  FOLD ? kSatFoldDz : 511>::BYTES;
 }
 template <int R, int PLANES, int MAXW, int P, bool FOLD>
 constexpr int pick_waves_sat() {
@@ -383,8 +378,6 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     }
     if constexpr (JOINT && R <= kSatMaxR)  // saturating-address folded tables (SatLut)
         if (a.fold && a.lut_nonzero <= SatLut<R, 0>::DZ) return launch_bilateral_ne<R, JOINT, FMA, 32, true, true>(a, stream);
-    if constexpr (JOINT && R <= kFoldMaxR)
-        if (a.fold) return launch_bilateral_ne<R, JOINT, FMA, 32, true>(a, stream);
     if constexpr (JOINT && VIP_JBF_SHORT_LUT)
         if (a.lut_nonzero <= 31) return launch_bilateral_ne<R, JOINT, FMA, 32>(a, stream);
     return launch_bilateral_ne<R, JOINT, FMA, 768>(a, stream);

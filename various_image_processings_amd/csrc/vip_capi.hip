@@ -178,7 +178,7 @@ using namespace vip;
 struct vip_bilateral_s {
     int width, height, ksize, radius, numerics, lut_nonzero;
     float* d_color;
-    float* d_fold;  // joint kernel's folded tables (small sigma_color, radius <= kFoldMaxR), or null
+    float* d_fold;  // joint kernel's folded tables (small sigma_color, radius <= kSatMaxR), or null
     RtTables rt;    // runtime-radius kernel tables
     float wsq[kWsStride * kWsStride];
 };
@@ -325,13 +325,14 @@ int vip_event_synchronize(void* event) { return (int)hipEventSynchronize((hipEve
 
 // ---------------------------------------------------------------- bilateral
 // Folded joint-kernel tables: table t (the t-th distinct r^2 of the disc, ascending)
-// entry d = RN(ws(r^2) * wc[d]) for d < 32 -- the product the kernel's unfolded taps
-// form (one float multiply), so results are unchanged. Needs wc[31..767] == 0.
+// entry d = RN(ws(r^2) * wc[d]) for d < kFoldEntries -- the product the kernel's unfolded
+// taps form (one float multiply), so results are unchanged. The kernel reads them behind
+// the saturating address (SatLut) when wc is zero from its DZ on.
 static int upload_fold(vip_bilateral_s* h, float sigma_color) {
     const int R = h->radius;
     float wc[768];
     build_color(768, sigma_color, h->numerics, wc);
-    float fold[(kFoldTablesMaxR * kFoldTablesMaxR + 1) * 32];
+    float fold[(kSatMaxR * kSatMaxR + 1) * kFoldEntries];
     int ntab = 0;
     for (int v = 0; v <= R * R; ++v) {
         if (!is_disc_r2(R, v)) continue;
@@ -339,11 +340,11 @@ static int upload_fold(vip_bilateral_s* h, float sigma_color) {
         for (int y = 0; y <= R; ++y)
             for (int x = 0; x <= R; ++x)
                 if (x * x + y * y == v) ws = h->wsq[y * kWsStride + x];
-        for (int d = 0; d < 32; ++d) fold[ntab * 32 + d] = wc[d] * ws;
+        for (int d = 0; d < kFoldEntries; ++d) fold[ntab * kFoldEntries + d] = wc[d] * ws;
         ++ntab;
     }
-    VIP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->d_fold), sizeof(float) * 32 * ntab));
-    VIP_HIP_CHECK(hipMemcpy(h->d_fold, fold, sizeof(float) * 32 * ntab, hipMemcpyHostToDevice));
+    VIP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&h->d_fold), sizeof(float) * kFoldEntries * ntab));
+    VIP_HIP_CHECK(hipMemcpy(h->d_fold, fold, sizeof(float) * kFoldEntries * ntab, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -361,7 +362,7 @@ int vip_bilateral_create(vip_bilateral_t* out, int width, int height, int ksize,
     build_space_q(h->radius, sigma_space, h->numerics, h->wsq);
     int rc = upload_color(&h->d_color, 768, sigma_color, h->numerics, &h->lut_nonzero);
     if (!rc) rc = upload_rt_tables(h->radius, sigma_space, h->numerics, &h->rt);
-    if (!rc && h->lut_nonzero <= 31 && h->radius <= kFoldTablesMaxR) rc = upload_fold(h, sigma_color);
+    if (!rc && h->lut_nonzero < kFoldEntries && h->radius <= kSatMaxR) rc = upload_fold(h, sigma_color);
     if (rc) {
         vip_bilateral_destroy(h);
         return rc;

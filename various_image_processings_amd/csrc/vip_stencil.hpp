@@ -25,15 +25,19 @@ constexpr int kWsStride = kMaxRadius + 1; // spatial weights stored as ws[|ky|][
 constexpr int kP = 8;                     // outputs per thread
 constexpr int kTW = 16 * kP;              // tile width in pixels
 constexpr int kLdsBudget = 160 * 1024;
-#ifndef VIP_JBF_FOLD_MAX_R  // joint kernel: folded per-r^2 colour x space tables up to this radius
-#define VIP_JBF_FOLD_MAX_R 0
-#endif
-constexpr int kFoldMaxR = VIP_JBF_FOLD_MAX_R;
 #ifndef VIP_JBF_SAT_MAX_R  // joint kernel: folded tables behind a saturating address (SatLut) up to this radius
 #define VIP_JBF_SAT_MAX_R 6
 #endif
 constexpr int kSatMaxR = VIP_JBF_SAT_MAX_R;
-constexpr int kFoldTablesMaxR = kFoldMaxR > kSatMaxR ? kFoldMaxR : kSatMaxR;  // handles upload the tables
+constexpr int kFoldEntries = 32;  // the handle's folded tables hold d < 32 (zeros past the colour LUT's end)
+// Largest distance the folded SatLut stores (measurement knob). A larger DZ (51 at R = 4,
+// with 64-entry tables) means fewer saturated lanes and fewer 2-way conflicts on copy 31's
+// bank, but measured no faster: C4 frame 674.8 -> 678.9 us (profiles/r03_sat_variants.txt).
+#ifndef VIP_JBF_SAT_DZMAX
+#define VIP_JBF_SAT_DZMAX (kFoldEntries - 1)
+#endif
+constexpr int kSatFoldDz = VIP_JBF_SAT_DZMAX;
+static_assert(kSatFoldDz < kFoldEntries, "folded tables hold d < kFoldEntries");
 
 // Folded joint-bilateral LUT behind a saturating address (SAT). One table per distinct
 // squared tap distance r^2 (NTAB of them) holds RN(ws(r^2) * wc[d]), 32 interleaved
@@ -43,7 +47,9 @@ constexpr int kFoldTablesMaxR = kFoldMaxR > kSatMaxR ? kFoldMaxR : kSatMaxR;  //
 // compile-time T - B0 + 128k in the ds_read immediate. Up to d = DZ that is the entry
 // itself; every larger d saturates to 65535, which B0 = 65535 - DZ*S - 124 places on entry
 // (DZ, k, 31) -- an exact zero whenever the colour LUT is zero from DZ on (the texture
-// filter's sigma_color sqrt(3): zero from d = 25). So the clamp costs no instruction and
+// filter's sigma_color sqrt(3): zero from d = 25; DZ = 31 at R <= 5, 26 at R = 6). A
+// saturated lane reads the bank of copy 31: a 2-way conflict when that lane does not
+// saturate. So the clamp costs no instruction and
 // the spatial multiply is folded away: per tap v_sad_u8, v_mad_legacy_u16, ds_read,
 // 3 v_fma, v_add (the 32-copy reads stay bank-conflict free; lanes that saturate read one
 // broadcast word). T = B0 rounded up to 16 keeps the immediate small and >= 0; the tile
@@ -51,11 +57,11 @@ constexpr int kFoldTablesMaxR = kFoldMaxR > kSatMaxR ? kFoldMaxR : kSatMaxR;  //
 // NTAB_ = 1, DZMAX = 511: the unfolded colour LUT of the plain filter (zero from d <= 511,
 // e.g. sigma_color 30: zero from 432) as 512 entries x 32 copies -- 64 KiB instead of 96,
 // the v_lshl_or of the address replaced by the (fast-class) v_mad_legacy_u16.
-template <int R, int PB, int NTAB_ = disc_r2_count(R), int DZMAX = 31>
+template <int R, int PB, int NTAB_ = disc_r2_count(R), int DZMAX = kSatFoldDz>
 struct SatLut {
     static constexpr int NTAB = NTAB_;
     static constexpr int S = NTAB * 128;
-    static constexpr int DZ = (65535 - 124) / S < DZMAX ? (65535 - 124) / S : DZMAX;  // fold tables hold d < 32
+    static constexpr int DZ = (65535 - 124) / S < DZMAX ? (65535 - 124) / S : DZMAX;  // tables hold d <= DZMAX
     static constexpr int B0 = 65535 - DZ * S - 124;
     static constexpr int T = round_up(B0, 16);
     static constexpr int PL = PB <= B0 ? 0 : round_up(T + (DZ + 1) * S, 16);  // plane offset
@@ -78,7 +84,7 @@ struct StencilArgs {
     int dst_aligned;       // dst base and pitch are 8-byte aligned -> qword stores
     const float* color;    // colour LUT in device memory
     int lut_nonzero;       // entries [lut_nonzero, end) of the colour LUT are exactly 0
-    const float* fold;     // or null: [disc_r2_count(R)][32] = RN(ws(r^2) * colour[d]), d < 32
+    const float* fold;     // or null: [disc_r2_count(R)][kFoldEntries] = RN(ws(r^2) * colour[d])
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 
@@ -344,7 +350,7 @@ struct LutStage {
     }
 };
 
-// SatLut staging: the fold tables ([NTAB][32] in device memory, d < 32) into the
+// SatLut staging: the fold tables ([NTAB][kFoldEntries] in device memory) into the
 // [d][table][copy] layout, d = 0..DZ, at LDS byte T (the store() argument points there).
 template <int NT, class SL>
 struct SatStage {
@@ -358,7 +364,7 @@ struct SatStage {
         for (int k = 0; k < K; ++k) {
             const int q = (int)threadIdx.x + k * NT;
             const int w = 4 * q, d = w / WPD, t = (w - d * WPD) >> 5;
-            if (N % NT == 0 || q < N) v[k] = __float_as_uint(fold[t * 32 + d]);
+            if (N % NT == 0 || q < N) v[k] = __float_as_uint(fold[t * kFoldEntries + d]);
         }
     }
     __device__ __forceinline__ void store(uint32_t* lut) const {
