@@ -300,6 +300,13 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms)
             jtraffic, jsrc = pmc_traffic(config, [jbf_k])
             out.update(bound="valu-fp32", achieved=jbf["achieved"], peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                        frac=jbf["frac"], traffic=jtraffic, traffic_source=jsrc, traffic_algorithmic=9.0 * px)
+        elif guide["valu_issue"]:
+            # the guide stage moves 6 B/px (0.1 of HBM): its roof is the VALU issue rate
+            # (DESIGN.md section 4), with the HBM figures beside it
+            vi = guide["valu_issue"]
+            out.update(bound="valu-issue", achieved=vi["achieved"], peak=vi["peak"], unit=vi["unit"], frac=vi["frac"],
+                       hbm=guide["hbm"], traffic=guide["hbm"]["traffic"],
+                       traffic_source=guide["hbm"]["traffic_source"], traffic_algorithmic=6.0 * px)
         else:
             out.update(bound="hbm", achieved=guide["hbm"]["achieved"], peak=PEAK_HBM_GBS, unit="GB/s",
                        frac=guide["hbm"]["frac"], traffic=guide["hbm"]["traffic"], traffic_source=guide["hbm"]["traffic_source"],
