@@ -68,11 +68,20 @@ namespace vip {
 // attribute is per device and one process may drive several). `devs` is the
 // caller's per-kernel static bitmask; concurrent first calls set it twice, which
 // is harmless.
-inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned long long>& devs) {
+// ABS_LDS: the kernel addresses LDS absolutely (the SatLut tables: a constant byte offset
+// in the ds_read immediate), which holds only while its dynamic LDS starts at byte 0, i.e.
+// the kernel has no static LDS; checked once, a kernel with any is refused (hipErrorInvalidKernelFile).
+inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned long long>& devs,
+                              bool abs_lds = false) {
     int dev = 0;
     VIP_HIP_CHECK(hipGetDevice(&dev));
     const unsigned long long bit = 1ull << (dev & 63);
     if (devs.load(std::memory_order_relaxed) & bit) return 0;
+    if (abs_lds) {
+        hipFuncAttributes fa{};
+        VIP_HIP_CHECK(hipFuncGetAttributes(&fa, kern));
+        if (fa.sharedSizeBytes != 0) return (int)hipErrorInvalidKernelFile;
+    }
     VIP_HIP_CHECK(hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
     devs.fetch_or(bit, std::memory_order_relaxed);
     return 0;
