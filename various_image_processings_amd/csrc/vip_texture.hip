@@ -679,7 +679,9 @@ VIP_GF_STAMP(8);
         // as the reference's strict > scan. Every rtv is <= 255 < the scan's initial 1e10f
         // (FLT_MAX in the CPP profile), so that initial value never survives.
         uint32_t rv[kGfRun + 2 * R];
+#ifndef VIP_GF_ARGMIN_LATE
         int ri[kGfRun + 2 * R];
+#endif
 #pragma unroll
         for (int t = 0; t < kGfRun + 2 * R; ++t) {  // window rows ty0-R .. ty0+kGfRun-1+R
             const float* row = RR + (ty0 + t) * G::BW + tx;
@@ -689,11 +691,13 @@ VIP_GF_STAMP(8);
             uint32_t v = m[0];
 #pragma unroll
             for (int kx = 1; kx < K; ++kx) v = v < m[kx] ? v : m[kx];
+            rv[t] = v;
+#ifndef VIP_GF_ARGMIN_LATE
             int c = K - 1;
 #pragma unroll
             for (int kx = K - 2; kx >= 0; --kx) c = m[kx] == v ? kx : c;
-            rv[t] = v;
             ri[t] = (ty0 + t) * G::BW + tx + c;
+#endif
         }
 #pragma unroll
         for (int j = 0; j < kGfRun; ++j) {
@@ -703,9 +707,23 @@ VIP_GF_STAMP(8);
             uint32_t mb = rv[j];
 #pragma unroll
             for (int ky = 1; ky < K; ++ky) mb = mb < rv[j + ky] ? mb : rv[j + ky];
+#ifndef VIP_GF_ARGMIN_LATE
             int mi = ri[j + K - 1];
 #pragma unroll
             for (int ky = K - 2; ky >= 0; --ky) mi = rv[j + ky] == mb ? ri[j + ky] : mi;
+#else  // measurement knob: row minima only; the argmin's row, then its column, per output
+            int roff = (j + K - 1) * G::BW;
+#pragma unroll
+            for (int ky = K - 2; ky >= 0; --ky) roff = rv[j + ky] == mb ? (j + ky) * G::BW : roff;
+            const int rowi = ty0 * G::BW + tx + roff;
+            uint32_t mm[K];
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) mm[kx] = __float_as_uint(RR[rowi + kx]);
+            int c = K - 1;
+#pragma unroll
+            for (int kx = K - 2; kx >= 0; --kx) c = mm[kx] == mb ? kx : c;
+            const int mi = rowi + c;
+#endif
             const float rmin = __uint_as_float(mb);
 #else  // the reference's scan: compare and select per position
         float rv[kGfRun + 2 * R];
