@@ -289,6 +289,13 @@ struct TilePrefetch {
             const int sy = clampi(ty0 + a.src_row0 - R + r, a.row_lo, a.row_hi - 1);
             const uint8_t* row = img + (long long)sy * pitch;
             const int x = tx0 - G::L + 4 * gc;
+#ifdef VIP_ABL_NOLOAD  // timing ablation only (wrong output): no HBM reads, the apron included
+            if (true) {
+                raw[k][0] = (uint32_t)g * 0x01030507u;
+                raw[k][1] = (uint32_t)(g + x) * 0x07050301u;
+                raw[k][2] = (uint32_t)(g ^ sy) * 0x01010101u;
+            } else
+#endif
             if (a.aligned && x >= 0 && x + 3 < a.width) {
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
                 raw[k][0] = w[0];
