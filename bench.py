@@ -508,6 +508,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
         if native:
             nrun = sb.launcher()  # vip_shard_run with its arguments bound
+            nbatch = sb.batch_launcher()  # vip_shard_run_batch: several frames' halos in one RCCL group
 
             def run(i, s=stream, h=0):  # exchange + filter (vip_shard_run)
                 nrun(sp[i % NBUF], dp[i % NBUF], sraw[h])
@@ -528,12 +529,33 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     # native -- vip_shard_run_timed's run start, halos in, interior done, edges done.
     marks = []
     group = state.get("torch_group")
+    # native N > 1: frames may share one RCCL group per B frames (vip_shard_run_batch; the
+    # group's cost is mostly fixed, profiles/r03_rccl_enqueue.txt). Frame i then runs on
+    # stream (i // B) % S; B * S divides NBUF, so buffer i % NBUF still always meets the
+    # same stream and a halo receive into it stays ordered after its last reader.
+    hb = dict(B=1, pending=[])
+
+    def flush():
+        if hb["pending"]:
+            i0 = hb["pending"][0]
+            nbatch([sp[j % NBUF] for j in hb["pending"]], [dp[j % NBUF] for j in hb["pending"]],
+                   sraw[(i0 // hb["B"]) % S])
+            hb["pending"].clear()
 
     def step(i, sample=False):
         # step i on stream i % S; buffer i % NBUF therefore always meets the same stream
         # (S divides NBUF), so a halo receive into it is ordered after its last reader
         h = 0 if sample else i % S
         s = streams[h]
+        if native and not sample and hb["B"] > 1:
+            # batches end on multiples of B (a phase end flushes a partial one), so every
+            # frame of a batch has the same i // B, hence the same stream
+            hb["pending"].append(i)
+            if (i + 1) % hb["B"] == 0:
+                flush()
+            return
+        if native and sample:
+            flush()
         if not multi and not sample:  # one GPU: the launch names its stream; no torch stream context
             run(i, s, h)
             return
@@ -585,34 +607,46 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     if native:
         # vip_shard_set_split: interior rows under the exchange then the two edge bands,
         # or one launch after the exchange (fewer launches; with two frames in flight the
-        # exchange still overlaps the other frame's kernel). Which is faster depends on the
-        # exchange's latency on this machine: time both (max over ranks) and keep the faster.
+        # exchange still overlaps the other frame's kernel); and B frames per RCCL group.
+        # Which is faster depends on the exchange's latency and host cost on this machine:
+        # time each (max over ranks) and keep the fastest.
         trial = {}
-        n_trial = 40
+        n_trial = 42  # a multiple of every B
+        batches = [b for b in (1, 2, 3) if NBUF % (b * S) == 0]
         for split in (True, False):
-            sb.set_split(split)
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            t0 = time.perf_counter()
-            for _ in range(n_trial):
-                step(i_settle)
-                i_settle += 1
-            torch.cuda.synchronize(dev)
-            dist.barrier()
-            dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
-            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            trial[split] = float(dt[0])
-        best = min(trial, key=trial.get)
-        sb.set_split(best)
-        res["exchange"] += ("; interior rows overlapped with the exchange, then the edge bands" if best
+            for b in batches:
+                sb.set_split(split)
+                hb["B"] = b
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                t0 = time.perf_counter()
+                for _ in range(n_trial):
+                    step(i_settle)
+                    i_settle += 1
+                flush()
+                torch.cuda.synchronize(dev)
+                dist.barrier()
+                dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
+                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+                trial[(split, b)] = float(dt[0])
+        best_split, best_b = min(trial, key=trial.get)
+        sb.set_split(best_split)
+        hb["B"] = best_b
+        res["exchange"] += ("; interior rows overlapped with the exchange, then the edge bands" if best_split
                             else "; one launch over the own rows after the exchange")
-        res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best
+        if best_b > 1:
+            res["exchange"] += f"; the halos of {best_b} frames per RCCL group"
+        res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best_split
                             else "one launch after the exchange",
-                            trial_ms_per_step={"split": round(trial[True], 4), "one_launch": round(trial[False], 4)})
+                            trial_ms_per_step={("split" if sp_ else "one_launch") + (f"_batch{b}" if b > 1 else ""):
+                                               round(v, 4) for (sp_, b), v in trial.items()})
+        res["halo_batch"] = best_b
     res["settle_steps"] = i_settle
     base = i_settle
     for i in range(args.warmup):
         step(base + i)
+    if native:
+        flush()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -624,6 +658,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         s.wait_event(ev0)
     for i in range(args.steps):
         step(base + args.warmup + i)
+    if native:
+        flush()  # a partial last batch is part of the timed frames
     for s in streams[1:]:
         stream.wait_stream(s)
     ev1.record(stream)
@@ -833,6 +869,7 @@ def main():
         "settle": {"seconds": args.settle_s, "steps": m["settle_steps"]},
         **{k_: round(v, 4) for k_, v in parts.items()},
         **({"split": m["split"]} if m.get("split") else {}),
+        **({"halo_batch": m["halo_batch"]} if m.get("halo_batch") else {}),
         **({"weak": weak} if weak else {}),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

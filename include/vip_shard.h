@@ -124,6 +124,13 @@ int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pit
 int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream,
                         void* const* events);
 
+/* vip_shard_run for n frames at once (slabs[i] -> outs[i]): the halos of all n frames move
+ * in ONE RCCL group (its host and device cost is mostly per group: 4 ops ~30 us, 12 ops
+ * ~36 us on one MI355X, microbench/rccl_enqueue.hip), then the n filter launches follow
+ * on `stream`. Every rank must batch the same frames in the same order. */
+int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* const* d_outs, size_t out_pitch,
+                        void* stream);
+
 /* One filter application of every shard of a group created by vip_shard_create_group
  * (one process): slabs[i], outs[i] (pitch out_pitch) and streams[i] on shard i's device. */
 int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* const* outs, size_t out_pitch,

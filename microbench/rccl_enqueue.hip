@@ -42,14 +42,17 @@ int main() {
     CK(hipMalloc(&a, 4 * bytes));
     CK(hipMalloc(&b, 4 * bytes));
     CK(hipMalloc(&f, 1 << 20));
+    int frames = 1;  // frames whose halos share one group (2 sends + 2 receives each)
     auto exchange = [&]() -> int {
         CK(hipEventRecord(ev_in, s));
         CK(hipStreamWaitEvent(c, ev_in, 0));
         CK(ncclGroupStart());
-        CK(ncclSend(a, bytes, ncclUint8, 0, comm, c));
-        CK(ncclRecv(b, bytes, ncclUint8, 0, comm, c));
-        CK(ncclSend(a + bytes, bytes, ncclUint8, 0, comm, c));
-        CK(ncclRecv(b + bytes, bytes, ncclUint8, 0, comm, c));
+        for (int fr = 0; fr < frames; ++fr) {
+            CK(ncclSend(a + 2 * fr * bytes, bytes, ncclUint8, 0, comm, c));
+            CK(ncclRecv(b + 2 * fr * bytes, bytes, ncclUint8, 0, comm, c));
+            CK(ncclSend(a + (2 * fr + 1) * bytes, bytes, ncclUint8, 0, comm, c));
+            CK(ncclRecv(b + (2 * fr + 1) * bytes, bytes, ncclUint8, 0, comm, c));
+        }
         CK(ncclGroupEnd());
         CK(hipEventRecord(ev_x, c));
         CK(hipStreamWaitEvent(s, ev_x, 0));
@@ -78,6 +81,26 @@ int main() {
         std::printf("%-40s host enqueue %.2f us per step, device %.2f us per step\n", name[mode], host_us / n,
                     ms * 1e3 / n);
     }
+    for (frames = 2; frames <= 4; frames *= 2) {  // one group for several frames' halos
+        for (int w = 0; w < 50; ++w)
+            if (exchange()) return 1;
+        CK(hipStreamSynchronize(s));
+        const int n = 1000;
+        double host_us = 0;
+        CK(hipEventRecord(t0, s));
+        for (int i = 0; i < n; ++i) {
+            const auto h0 = std::chrono::steady_clock::now();
+            if (exchange()) return 1;
+            host_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count();
+        }
+        CK(hipEventRecord(t1, s));
+        CK(hipEventSynchronize(t1));
+        float ms = 0;
+        CK(hipEventElapsedTime(&ms, t0, t1));
+        std::printf("one group for %d frames' halos (%d ops)     host enqueue %.2f us per group, device %.2f us per group\n",
+                    frames, 4 * frames, host_us / n, ms * 1e3 / n);
+    }
+    frames = 1;
     // the same step captured once into a hipGraph (exchange on the joined communication
     // stream, then the launch) and replayed: host cost of hipGraphLaunch per step
     {

@@ -165,6 +165,31 @@ def test_rccl_single_rank_native_shard_timed(dev, oracle):
         assert ev[0].elapsed_time(ev[3]) > 0
 
 
+def test_rccl_single_rank_batch(dev, oracle):
+    """vip_shard_run_batch on a one-rank communicator: three frames (different images) in
+    one call, each equal to its own single launch, in both split modes."""
+    img = [oracle.random_image(900, 500) if f == 0 else np.ascontiguousarray(oracle.random_image(900, 500)[::-1])
+           for f in range(2)]
+    img.append(np.ascontiguousarray(img[0][:, ::-1]))
+    s = NativeShard(900, 500, 15, 0, 1, native_unique_id())
+    geo = s.geo
+    slabs, outs = [], []
+    for im in img:
+        sl = dev.empty((geo.slab_rows, 900, 3))
+        sl[geo.radius:geo.radius + geo.own] = dev.put(im)
+        slabs.append(sl)
+        outs.append(dev.empty((500, 900, 3)))
+    run = s.batch_launcher()
+    for split in (True, False):
+        s.set_split(split)
+        for o in outs:
+            o.zero_()
+        run([t.data_ptr() for t in slabs], [t.data_ptr() for t in outs], dev.torch_.cuda.current_stream().cuda_stream)
+        dev.torch_.cuda.synchronize()
+        for im, o in zip(img, outs):
+            assert np.array_equal(dev.get(o), _single(dev, im, 15, False))
+
+
 def test_rccl_missing_peer_times_out():
     """A 2-rank communicator whose second rank never joins: vip_shard_create returns
     VIP_ERR_COMM_TIMEOUT after its timeout instead of blocking (run in a child process

@@ -33,6 +33,7 @@ SIGNATURES = {
     "vip_shard_set_split": (_i, [_p, _i]),
     "vip_shard_run": (_i, [_p, _p, _p, _s, _p]),
     "vip_shard_run_timed": (_i, [_p, _p, _p, _s, _p, _pp]),
+    "vip_shard_run_batch": (_i, [_p, _i, _pp, _pp, _s, _p]),
     "vip_shard_run_group": (_i, [_pp, _i, _pp, _pp, _s, _pp]),
     "vip_shard_last_error": (ctypes.c_char_p, []),
     "vip_shard_destroy": (_i, [_p]),

@@ -482,6 +482,43 @@ static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
     return rc;
 }
 
+int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* const* d_outs, size_t out_pitch,
+                        void* stream) {
+    if (!h || n <= 0 || !d_slabs || !d_outs || out_pitch < h->pitch() || h->transport != VIP_SHARD_RCCL || !h->nccl)
+        return VIP_ERR_INVALID_ARGUMENT;
+    for (int f = 0; f < n; ++f)
+        if (!d_slabs[f] || !d_outs[f]) return VIP_ERR_INVALID_ARGUMENT;
+    DeviceGuard guard;
+    const hipStream_t s = (hipStream_t)stream;
+    VIP_HIP_TRY(hipSetDevice(h->device));
+    if (!h->above() && !h->below()) {  // no neighbours: the launches only
+        for (int f = 0; f < n; ++f)
+            if (const int rc = filter_rows(h, d_slabs[f], d_outs[f], out_pitch, 0, h->own, s)) return rc;
+        return 0;
+    }
+    // every frame's own rows written -> one group with all the halos on the communication stream
+    VIP_HIP_TRY(hipEventRecord(h->ev_in, s));
+    VIP_HIP_TRY(hipStreamWaitEvent(h->comm, h->ev_in, 0));
+    int rc = 0;
+    if (const ncclResult_t e = ncclGroupStart()) return comm_fail(e, "ncclGroupStart");
+    for (int f = 0; f < n && !rc; ++f) rc = enqueue_p2p(h, d_slabs[f]);
+    const int rc2 = group_end(&h, 1);
+    if (rc || rc2) return rc ? rc : rc2;
+    VIP_HIP_TRY(hipEventRecord(h->ev_x, h->comm));
+    if (!h->split) {
+        VIP_HIP_TRY(hipStreamWaitEvent(s, h->ev_x, 0));
+        for (int f = 0; f < n; ++f)
+            if ((rc = filter_rows(h, d_slabs[f], d_outs[f], out_pitch, 0, h->own, s))) return rc;
+        return 0;
+    }
+    for (int f = 0; f < n; ++f)  // interiors under the exchange, then every frame's edge bands
+        if ((rc = interior(h, d_slabs[f], d_outs[f], out_pitch, s))) return rc;
+    VIP_HIP_TRY(hipStreamWaitEvent(s, h->ev_x, 0));
+    for (int f = 0; f < n; ++f)
+        if ((rc = edges(h, d_slabs[f], d_outs[f], out_pitch, s))) return rc;
+    return 0;
+}
+
 int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream) {
     DeviceGuard guard;
     return shard_run(h, d_slab, d_out, out_pitch, stream, nullptr);

@@ -359,6 +359,22 @@ class NativeShard:
                 raise S.ShardError("vip_shard_run", rc)
         return run
 
+    def batch_launcher(self):
+        """A lean callable f(slab_ptrs, out_ptrs, hip_stream) for vip_shard_run_batch: the
+        halos of all the frames in one RCCL group, then their launches (raw device
+        addresses, unchecked). Every rank must batch the same frames."""
+        import ctypes
+        from . import _shard_lib as S
+        fn = S.lib().vip_shard_run_batch
+        h, p = self._h, self.geo.width * 3
+
+        def run(slabs, outs, stream):
+            n = len(slabs)
+            rc = fn(h, n, (ctypes.c_void_p * n)(*slabs), (ctypes.c_void_p * n)(*outs), p, stream)
+            if rc:
+                raise S.ShardError("vip_shard_run_batch", rc)
+        return run
+
     def filter_timed(self, slab, out, events, stream=None) -> None:
         """events: 4 timing-enabled torch.cuda.Event (vip_shard_run_timed): run start,
         halos received (communication stream), interior done, edges done."""
