@@ -46,6 +46,14 @@ PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (== f32 MFMA) pe
 VALU_SIMDS = 1024            # 256 CUs x 4 SIMDs
 VALU_CYCLES_PER_INSTR = 2    # a wave64 VALU instruction issues over 2 cycles (MI355X_MICROARCH.md)
 NBUF = 12
+
+
+def halo_batches(streams: int) -> list:
+    """Frames per RCCL group the N > 1 native path may use with this many streams: frame i
+    runs in batch i // B on stream (i // B) % S, so B * S must divide NBUF for buffer
+    i % NBUF to always meet the same stream (its halo receive then stays ordered after its
+    last reader)."""
+    return [b for b in (1, 2, 3) if NBUF % (b * streams) == 0]
 BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
 
 
@@ -612,7 +620,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         # time each (max over ranks) and keep the fastest.
         trial = {}
         n_trial = 42  # a multiple of every B
-        batches = [b for b in (1, 2, 3) if NBUF % (b * S) == 0]
+        batches = halo_batches(S)
         for split in (True, False):
             for b in batches:
                 sb.set_split(split)

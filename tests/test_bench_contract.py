@@ -79,3 +79,16 @@ def test_committed_lines_time_the_roofline_on_one_stream():
         launch_ms = r["avg_launch_ms"] if cfg == "c2" else \
             [k["avg_launch_ms"] for k in (r["dominant"], r["other"]) if "guide" in k["kernel"]][0]
         assert abs(iso / 1e3 - launch_ms) / launch_ms < 0.03, (cfg, iso, launch_ms)
+
+
+def test_halo_batches_keep_buffers_on_one_stream():
+    """bench.py N > 1 native path: frame i in batch i // B on stream (i // B) % S. For
+    every batch size it may choose, each buffer (i % NBUF) always meets the same stream,
+    and every batch lies on one stream, for any frame count and any phase boundaries."""
+    for S in (1, 2, 3, 4, 6):
+        for B in bench.halo_batches(S):
+            seen = {}
+            for i in range(10 * bench.NBUF * B):
+                st = (i // B) % S
+                assert seen.setdefault(i % bench.NBUF, st) == st
+    assert bench.halo_batches(2) == [1, 2, 3]
