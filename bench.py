@@ -6,10 +6,12 @@
 
 One step = one filter application over each rank's row slab of a frame that is
 row-sharded across the N GPUs (one process per GPU, torch.distributed over
-RCCL/xGMI; N>1 is launched by torch.distributed.run). Each step the ranks exchange
-their r-row halos with the row neighbours only (include/vip_shard.h: ncclSend/ncclRecv
-on the library's own RCCL communicator, overlapped with the interior rows, whose
-windows need no halo; the edge bands follow).
+RCCL/xGMI). `python bench.py --gpus N` with N > 1 starts the N ranks itself (a child
+`python -m torch.distributed.run --nproc-per-node N ... bench.py`, before anything
+touches the GPU) and exits with its status; run under torch.distributed.run directly,
+each process is one rank. Each step the ranks exchange their r-row halos with the row
+neighbours only (include/vip_shard.h: ncclSend/ncclRecv on the library's own RCCL
+communicators, one per stream), then filter their own rows.
 
   c2 (default) bilateral r=7 (ksize 15, sigma_space 10, sigma_color 30) on the
      3840x2160 RGB8 frame, its rows split over the N ranks (strong scaling: BASELINE
@@ -18,7 +20,8 @@ windows need no halo; the edge bands follow).
   c3 adaptive bilateral r=7, same geometry (BASELINE config 3).
   c4 bilateral texture filter k=5, nitr=5 on 3840x2160 per rank (BASELINE config
      4); N>1 row-shards an (N*2160)x3840 frame with one 45-row halo exchange per
-     frame (sharded.ShardedTexture).
+     frame (vip_shard_create_texture; sharded.ShardedTexture over torch P2P for the
+     gloo rehearsal).
   c5 bilateral r=15 (ksize 31) on ONE 16384x16384 frame row-tiled over the N
      GPUs (strong scaling; BASELINE config 5).
 
@@ -46,6 +49,60 @@ PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (== f32 MFMA) pe
 VALU_SIMDS = 1024            # 256 CUs x 4 SIMDs
 VALU_CYCLES_PER_INSTR = 2    # a wave64 VALU instruction issues over 2 cycles (MI355X_MICROARCH.md)
 NBUF = 12
+
+
+LAUNCH_TIMEOUT_S = 1500.0  # whole N-rank run, launcher included
+
+
+def free_port() -> int:
+    """A TCP port on 127.0.0.1 that was free a moment ago (the rendezvous of the ranks)."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_argv(n: int, argv: list, port: int, script: str | None = None) -> list:
+    """The child command `python bench.py --gpus N` runs when it is not itself a rank: the
+    driver's own form, python -m torch.distributed.run --nnodes=1 --nproc-per-node N
+    --master-addr 127.0.0.1 --master-port P bench.py <the same arguments>. torchrun gives
+    each rank RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR and MASTER_PORT."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", script or os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script: str | None = None) -> int:
+    """Run N rank processes (one per GPU) as a child torchrun and return its exit status.
+
+    Called before anything touches the GPU (this process only parsed its arguments), and
+    the ranks are children, never an exec of this process. The ranks inherit stdout, so
+    rank 0's JSON line is this command's output. Non-zero when any rank fails (torchrun's
+    status); 124 when the whole run exceeds timeout_s, after its process group -- the
+    launcher and every rank it started -- has been terminated (SIGTERM, then SIGKILL after
+    10 s)."""
+    import signal
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the host driver supports dmabuf IPC only
+    cmd = rank_launch_argv(n, argv, free_port(), script)
+    print(f"bench.py: --gpus {n}: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        return proc.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        print(f"bench.py: the {n}-rank run did not finish in {timeout_s:.0f} s; terminating it", file=sys.stderr,
+              flush=True)
+        for sig, grace in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(proc.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                proc.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        return 124
 
 
 def halo_batches(streams: int) -> list:
@@ -141,6 +198,14 @@ def parse():
     p.add_argument("--exchange", default=None, choices=["native", "torch"])
     # rehearsal of the N > 1 native path in ONE process (a one-rank RCCL communicator)
     p.add_argument("--rehearse-native", action="store_true")
+    # with --rehearse-native: this rank's slab of an N-way row split, whose two row neighbours
+    # are the rank itself over a one-rank RCCL communicator (vip_shard_create_loopback), so
+    # the real exchange, its trial forms and graph replay run on one GPU. One rank's slab:
+    # not a scaling number.
+    p.add_argument("--loopback", type=int, default=0, metavar="N")
+    # --gpus N > 1 without WORLD_SIZE in the environment: this process starts the N ranks
+    # itself (a child torchrun) and ends them after this many seconds
+    p.add_argument("--launch-timeout", type=float, default=LAUNCH_TIMEOUT_S)
     return p.parse_args()
 
 
@@ -423,27 +488,37 @@ def init_distributed(args, rank, dev):
     return backend
 
 
-def native_shard(args, cfg, frame_h, rank, world):
-    """This rank's NativeShard (vip_shard_create over a communicator id from rank 0),
-    or (None, reason) when any rank failed to create it -- all ranks agree (gloo)."""
+def native_shards(args, cfg, frame_h, rank, world, n):
+    """This rank's n NativeShards, one per stream, each over its own RCCL communicator
+    (vip_shard_create / vip_shard_create_texture with a communicator id from rank 0): a
+    stream's exchanges then never share a communicator or a communication stream with the
+    other stream's, and a texture shard's scratch slabs serve one frame at a time. Returns
+    (shards, None), or (None, reason) when any rank failed -- all ranks agree (gloo)."""
     import torch
     import torch.distributed as dist
 
     from various_image_processings_amd.sharded import NativeShard, native_unique_id
-    box = [native_unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(box, src=0)
-    ns, err = None, ""
-    try:
-        ns = NativeShard(cfg["width"], frame_h, cfg["ksize"], rank, world, box[0], adaptive=cfg["kind"] == "adaptive",
-                         timeout_ms=120000)
-    except Exception as e:  # noqa: BLE001
-        err = f"rank {rank}: {e}"
-        print(f"bench.py {err}", file=sys.stderr, flush=True)
-    ok = torch.tensor([0 if ns is None else 1], dtype=torch.int32)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    if int(ok[0]) == 0:
-        return None, err or "another rank failed to create its shard"
-    return ns, None
+    shards, err = [], ""
+    for _ in range(n):
+        box = [native_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        ns = None
+        if not err:
+            try:
+                lb = args.loopback > 1  # rehearsal: the middle rank of an N-way split, itself as neighbours
+                ns = NativeShard(cfg["width"], frame_h, cfg["ksize"], args.loopback // 2 if lb else rank,
+                                 args.loopback if lb else world, box[0],
+                                 adaptive=cfg["kind"] == "adaptive", timeout_ms=120000,
+                                 nitr=cfg["nitr"] if cfg["kind"] == "texture" else None, loopback=lb)
+            except Exception as e:  # noqa: BLE001
+                err = f"rank {rank}: {e}"
+                print(f"bench.py {err}", file=sys.stderr, flush=True)
+        ok = torch.tensor([0 if ns is None else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok[0]) == 0:
+            return None, err or "another rank failed to create its shard"
+        shards.append(ns)
+    return shards, None
 
 
 def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
@@ -465,7 +540,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     cdev = dev if state.get("backend") == "nccl" else "cpu"  # control tensors of the process group
     multi = state.get("multi", world > 1)  # a process group is up (N > 1, or --rehearse-native)
 
-    if cfg["kind"] == "texture" and world == 1:
+    if cfg["kind"] == "texture" and world == 1 and not args.loopback:
         rows = frame_h
         geo = None
         # one handle per stream: a texture handle owns its ping-pong and guide frames
@@ -486,47 +561,52 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * cfg["nitr"] + 1)]
             texs[0].execute_timed(srcs[i % NBUF], dsts[i % NBUF], ev, stream=stream)
             smarks.append(ev)
-    elif cfg["kind"] == "texture":
-        # row-sharded frame: one halo exchange of nitr * texture_halo_rows(k) rows per
-        # frame, then shrinking ghost zones (sharded.ShardedTexture; one per stream: it
-        # owns scratch slabs)
-        sts = [ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world) for _ in range(S)]
-        geo = sts[0].geo
-        rows = geo.own
-        srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
-        dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
-
-        def run(i, s=stream, h=0):
-            sts[h].filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
     else:
-        ns = None
+        shards = None
         if multi and args.exchange == "native":
-            ns, why = native_shard(args, cfg, frame_h, rank, world)
-            if ns is None:  # fall back to torch.distributed P2P over a new RCCL group
+            # one shard (own RCCL communicator, own communication stream) per stream
+            shards, why = native_shards(args, cfg, frame_h, rank, world, S)
+            if shards is None:  # fall back to torch.distributed P2P over a new RCCL group
                 if "torch_group" not in state:
                     state["torch_group"] = dist.new_group(backend="nccl" if args.backend == "nccl" else "gloo")
                 res["exchange_fallback"] = why
-        native = ns is not None
-        # the handle holds only read-only LUTs: one serves every stream
-        sb = ns if native else ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
+        native = shards is not None
+        if native:
+            sb = shards[0]
+        elif cfg["kind"] == "texture":
+            # torch P2P: one halo exchange of nitr * texture_halo_rows(k) rows per frame,
+            # then shrinking ghost zones (sharded.ShardedTexture; one per stream: it owns
+            # scratch slabs)
+            sts = [ShardedTexture(w, frame_h, k, cfg["nitr"], rank, world) for _ in range(S)]
+            sb = sts[0]
+        else:
+            # the handle holds only read-only LUTs: one serves every stream
+            sb = ShardedBilateral(w, frame_h, k, rank, world, adaptive=cfg["kind"] == "adaptive")
         geo = sb.geo
         rows = geo.own
         srcs = make_frames(torch, args.data, geo.slab_rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
         if native:
-            nrun = sb.launcher()  # vip_shard_run with its arguments bound
-            nbatch = sb.batch_launcher()  # vip_shard_run_batch: several frames' halos in one RCCL group
+            nruns = [x.launcher() for x in shards]  # vip_shard_run with its arguments bound
+            # vip_shard_run_batch: several frames' halos in one RCCL group
+            nbatches = [x.batch_launcher() for x in shards]
 
-            def run(i, s=stream, h=0):  # exchange + filter (vip_shard_run)
-                nrun(sp[i % NBUF], dp[i % NBUF], sraw[h])
+            def run(i, s=stream, h=0):  # exchange + filter (vip_shard_run) on stream h's shard
+                nruns[h](sp[i % NBUF], dp[i % NBUF], sraw[h])
+        elif cfg["kind"] == "texture":
+            def run(i, s=stream, h=0):
+                sts[h].filter(srcs[i % NBUF], dsts[i % NBUF], stream=s, exchange=False)
         else:
             launch = sb.launcher()  # the C entry point with its arguments bound
 
             def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
                 launch(sp[i % NBUF], dp[i % NBUF], sraw[h])
+    has_peers = world > 1 or (native and args.loopback > 1)
     res["exchange"] = (None if not multi else
-                       "native vip_shard (RCCL ncclSend/ncclRecv with the row neighbours)" if native else
+                       ("native vip_shard (RCCL ncclSend/ncclRecv with the row neighbours; one communicator per "
+                        "stream)" if has_peers else "native vip_shard, one rank: no neighbours, no exchange")
+                       if native else
                        f"torch.distributed P2P ({state.get('backend', args.backend)}), serial before the kernel")
 
     # N=1: the kernels run back to back and ev0..ev1 / steps is the kernel time per frame
@@ -545,9 +625,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
 
     def flush():
         if hb["pending"]:
-            i0 = hb["pending"][0]
-            nbatch([sp[j % NBUF] for j in hb["pending"]], [dp[j % NBUF] for j in hb["pending"]],
-                   sraw[(i0 // hb["B"]) % S])
+            h = (hb["pending"][0] // hb["B"]) % S
+            nbatches[h]([sp[j % NBUF] for j in hb["pending"]], [dp[j % NBUF] for j in hb["pending"]], sraw[h])
             hb["pending"].clear()
 
     def step(i, sample=False):
@@ -612,42 +691,67 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             step(i_settle)
             i_settle += 1
         torch.cuda.synchronize(dev)
-    if native:
+    if native and not has_peers:
+        # one rank (--rehearse-native): no halo moves, so split / batch forms would only
+        # time noise between identical launches; keep the defaults and say so
+        res["split"] = dict(chosen="one launch (no neighbours: no exchange, no trial)", trial_ms_per_step={})
+        res["split_on"] = False
+    elif native:
         # vip_shard_set_split: interior rows under the exchange then the two edge bands,
         # or one launch after the exchange (fewer launches; with two frames in flight the
         # exchange still overlaps the other frame's kernel); and B frames per RCCL group.
         # Which is faster depends on the exchange's latency and host cost on this machine:
-        # time each (max over ranks) and keep the fastest.
+        # time each (max over ranks) and keep the fastest. The texture filter has no split
+        # (every iteration reads the halo region).
+        # Graph mode (vip_shard_set_graph, one frame per captured graph, B = 1) replays each
+        # (buffer, stream)'s exchange + launches with one hipGraphLaunch: the per-frame host
+        # cost of an RCCL group (16-30 us, profiles/r03_rccl_enqueue.txt) against a rank's
+        # ~25 us C2 launch at N = 8 is what it removes.
         trial = {}
         n_trial = 42  # a multiple of every B
         batches = halo_batches(S)
-        for split in (True, False):
-            for b in batches:
-                sb.set_split(split)
-                hb["B"] = b
-                torch.cuda.synchronize(dev)
-                dist.barrier()
-                t0 = time.perf_counter()
-                for _ in range(n_trial):
-                    step(i_settle)
-                    i_settle += 1
-                flush()
-                torch.cuda.synchronize(dev)
-                dist.barrier()
-                dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
-                dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-                trial[(split, b)] = float(dt[0])
-        best_split, best_b = min(trial, key=trial.get)
-        sb.set_split(best_split)
+        forms = []
+        for split in ((False,) if cfg["kind"] == "texture" else (True, False)):
+            forms += [(split, b, False) for b in batches] + [(split, 1, True)]
+        for split, b, graph in forms:
+            for x in shards:
+                x.set_split(split)
+                x.set_graph(graph)
+            hb["B"] = b
+            for _ in range(NBUF):  # untimed: captures every (buffer, stream) graph in graph mode
+                step(i_settle)
+                i_settle += 1
+            flush()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(n_trial):
+                step(i_settle)
+                i_settle += 1
+            flush()
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            trial[(split, b, graph)] = float(dt[0])
+        best_split, best_b, best_graph = min(trial, key=trial.get)
+        res["split_on"] = best_split
+        for x in shards:
+            x.set_split(best_split)
+            x.set_graph(best_graph)
         hb["B"] = best_b
         res["exchange"] += ("; interior rows overlapped with the exchange, then the edge bands" if best_split
                             else "; one launch over the own rows after the exchange")
         if best_b > 1:
             res["exchange"] += f"; the halos of {best_b} frames per RCCL group"
+        if best_graph:
+            res["exchange"] += "; each frame replayed from a captured hipGraph"
         res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best_split
                             else "one launch after the exchange",
-                            trial_ms_per_step={("split" if sp_ else "one_launch") + (f"_batch{b}" if b > 1 else ""):
-                                               round(v, 4) for (sp_, b), v in trial.items()})
+                            graph=best_graph,
+                            trial_ms_per_step={("split" if sp_ else "one_launch") + (f"_batch{b_}" if b_ > 1 else "")
+                                               + ("_graph" if g_ else ""): round(v, 4)
+                                               for (sp_, b_, g_), v in trial.items()})
         res["halo_batch"] = best_b
     res["settle_steps"] = i_settle
     base = i_settle
@@ -668,6 +772,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         step(base + args.warmup + i)
     if native:
         flush()  # a partial last batch is part of the timed frames
+    host_s = time.perf_counter() - t0  # every step enqueued
     for s in streams[1:]:
         stream.wait_stream(s)
     ev1.record(stream)
@@ -685,7 +790,12 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         torch.cuda.synchronize(dev)
         avg = lambda a, b: sum(m[a].elapsed_time(m[b]) for m in marks) / len(marks)  # noqa: E731
         if native:
-            parts = dict(exchange_ms=avg(0, 1), interior_ms=avg(0, 2), edges_ms=avg(2, 3), run_ms=avg(0, 3))
+            # vip_shard_run_timed: events[2] after the interior rows (split) or once the
+            # halos are in on the filter stream (one launch)
+            if res.get("split_on"):
+                parts = dict(exchange_ms=avg(0, 1), interior_ms=avg(0, 2), edges_ms=avg(2, 3), run_ms=avg(0, 3))
+            else:
+                parts = dict(exchange_ms=avg(0, 1), wait_ms=avg(0, 2), filter_ms=avg(2, 3), run_ms=avg(0, 3))
             kernel_ms = parts["run_ms"]
         else:
             parts = dict(exchange_ms=avg(0, 1), kernel_ms=avg(1, 2))
@@ -705,8 +815,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             torch.cuda.synchronize(dev)
             single_ms = e0.elapsed_time(e1) / n1
     launch_ms = single_ms if single_ms is not None else kernel_ms
-    fused = cfg["kind"] == "texture" and world == 1 and args.texture_mode == "fused"
-    if cfg["kind"] == "texture" and world == 1 and not fused:
+    fused = cfg["kind"] == "texture" and world == 1 and not args.loopback and args.texture_mode == "fused"
+    if cfg["kind"] == "texture" and world == 1 and not args.loopback and not fused:
         # Per-stage split of the frame: an event between two launches costs a few us of
         # stream time (measured: +4 us on each stage against rocprofv3), so the timed
         # frames above carry no inner events; max(4, K/4) further frames, after the
@@ -721,13 +831,13 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         per = launch_ms / nit
         res["stage_ms"] = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
                            "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
-    keys = ["elapsed", "launch"] + (sorted(parts) if parts else [])
-    vals = [elapsed, launch_ms] + ([parts[x] for x in sorted(parts)] if parts else [])
+    keys = ["elapsed", "launch", "host"] + (sorted(parts) if parts else [])
+    vals = [elapsed, launch_ms, host_s] + ([parts[x] for x in sorted(parts)] if parts else [])
     t = torch.tensor(vals, dtype=torch.float64, device=cdev)
     if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     got = dict(zip(keys, (float(v) for v in t)))
-    res.update(elapsed=got["elapsed"], launch_ms=got["launch"], frame_ms=kernel_ms, rows=rows, geo=geo,
+    res.update(elapsed=got["elapsed"], launch_ms=got["launch"], host_s=got["host"], frame_ms=kernel_ms, rows=rows, geo=geo,
                parts={x: got[x] for x in sorted(parts)} if parts else None, native=native, fused=fused)
     return res
 
@@ -737,6 +847,9 @@ def main():
     if args.sample_table:
         sample_table(args)
         return
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.rehearse_native:
+        # plain `python bench.py --gpus N`: start the N ranks (nothing has touched the GPU)
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
     import torch
     import torch.distributed as dist
 
@@ -749,16 +862,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr,
+              flush=True)
     if args.same_device:
         local = 0
     if args.exchange is None:
         # the native RCCL exchange needs one GPU per rank; the one-GPU rehearsal (gloo,
         # every rank on cuda:0) keeps the torch P2P path
         args.exchange = "torch" if (args.same_device or args.backend == "gloo") else "native"
-    if cfg["kind"] == "texture":
-        args.exchange = "torch"  # the texture filter's wide halo goes through ShardedTexture
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     state = {"multi": world > 1 or args.rehearse_native}
@@ -781,8 +892,10 @@ def main():
     if "tiling" in cfg and world == 1:  # the config's tile shape (include/vip.h tuning knobs)
         vip.set_bilateral_waves(cfg["tiling"][0])
         vip.set_bilateral_wide(cfg["tiling"][1])
-    # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench)
-    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)]
+    # stream 0 is torch's current stream (S = 1 is exactly the single-stream bench); with
+    # a process group every stream is a created one (graph capture needs a non-null stream)
+    streams = ([torch.cuda.Stream(dev) for _ in range(S)] if state["multi"] else
+               [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(S - 1)])
     if args.scaling is None:
         # the metric's frame (3840x2160; C5 16384^2) split over the ranks; the texture
         # filter's 45-row ghost halo makes a split 4K frame mostly redundant work, so C4
@@ -791,7 +904,11 @@ def main():
     if "frame_height" in cfg:
         args.scaling = "strong"
     per_rank = cfg.get("rows_per_rank")
-    frame_h = cfg.get("frame_height") or (per_rank * world if args.scaling == "weak" else per_rank)
+    if args.loopback and not args.rehearse_native:
+        raise SystemExit("--loopback N is a --rehearse-native option")
+    gw = args.loopback if args.loopback > 1 else world  # ranks of the row split (geometry)
+    sharded = gw > 1  # this process filters a slab of a larger frame
+    frame_h = cfg.get("frame_height") or (per_rank * gw if args.scaling == "weak" else per_rank)
     m = measure(args, cfg, frame_h, torch, dev, rank, world, streams, state)
     weak = None
     if world > 1 and args.scaling == "strong" and per_rank and not args.no_weak:
@@ -807,7 +924,8 @@ def main():
     r = k // 2
     elapsed, launch_ms, rows, geo = m["elapsed"], m["launch_ms"], m["rows"], m["geo"]
     px_per_rank = rows * w
-    total_px = frame_h * w
+    # the whole frame's pixels (every rank's); a loopback rehearsal processes one slab only
+    total_px = px_per_rank if args.loopback > 1 else frame_h * w
     ms_per_step = elapsed / args.steps * 1e3
     value = total_px / (elapsed / args.steps) / 1e6
 
@@ -822,7 +940,7 @@ def main():
         hbm = 6.0 * px_per_rank / (launch_ms * 1e-3) / 1e9
         # the committed PMC summaries are single-GPU whole-frame launches
         kname = cfg.get("kernel", f"void vip::{cfg['kind']}_kernel<{r},")  # PMC summary lookup
-        traffic, tsrc = (None, None) if world > 1 else pmc_traffic(args.config, [kname])
+        traffic, tsrc = (None, None) if sharded else pmc_traffic(args.config, [kname])
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
@@ -832,7 +950,7 @@ def main():
                     gtaps_per_s=round(taps * px_per_rank / (launch_ms * 1e-3) / 1e9, 1),
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
                              bytes_per_px=6))
-        if world == 1:  # the committed PMC summaries are whole-frame launches
+        if not sharded:  # the committed PMC summaries are whole-frame launches
             roof["valu_issue"] = valu_issue(args.config, kname, launch_ms)
             if len(streams) > 1:  # the chip's rate with S frames in flight (launches overlap)
                 fl = flops / (ms_per_step * 1e-3) / 1e12
@@ -853,6 +971,9 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
+        # host time to enqueue the K timed steps (max over ranks), per step: below
+        # ms_per_step, the host keeps ahead of the GPU
+        "host_ms_per_step": round(m["host_s"] / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
@@ -860,7 +981,7 @@ def main():
         "data": DATA_DESC[args.data] + ", resident in HBM; f32 weights/sums",
         "config": {"workload": cfg["workload"], "ksize": k, "sigma_space": 10.0, "sigma_color": 30.0,
                    "frame": f"{w}x{frame_h}", "rows_per_rank": rows, "data": args.data,
-                   "parallelism": f"row-tiled x{world}" + (f" + {geo.radius}-row halo sendrecv" if world > 1 and geo else ""),
+                   "parallelism": f"row-tiled x{gw}" + (f" + {geo.radius}-row halo sendrecv" if sharded and geo else ""),
                    **({"tiling": cfg["kernel_label"]} if "tiling" in cfg and world == 1 else {}),
                    **({"texture_mode": args.texture_mode} if cfg["kind"] == "texture" and world == 1 else {}),
                    **({"backend": state.get("backend"), "exchange": m["exchange"]} if state["multi"] else {}),
@@ -880,7 +1001,11 @@ def main():
         **({"halo_batch": m["halo_batch"]} if m.get("halo_batch") else {}),
         **({"weak": weak} if weak else {}),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if args.loopback > 1:
+        out["rehearsal"] = (f"one GPU: the middle rank's slab of a {args.loopback}-way row split, its two neighbours "
+                            f"the rank itself over a one-rank RCCL communicator (vip_shard_create_loopback); value "
+                            f"counts this slab only -- not a scaling number")
+    if rank == 0 and not sharded and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(cfg)
         except Exception as e:  # the baseline is reported, never required

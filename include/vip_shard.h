@@ -117,10 +117,11 @@ int vip_shard_geometry(vip_shard_t h, int* row_begin, int* own_rows, int* halo_r
  * when `stream` is. Every rank must call it once per frame, in the same order. */
 int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream);
 
-/* As vip_shard_run, with timing events (hipEvent_t, timing enabled, as void*):
- * events[0] before the run on `stream`, events[1] after the exchange on the shard's
- * communication stream, events[2] after the interior rows on `stream`, events[3] after
- * the edge bands on `stream`. */
+/* As vip_shard_run (never from a graph), with timing events (hipEvent_t, timing enabled,
+ * as void*): events[0] before the run on `stream`, events[1] after the exchange on the
+ * shard's communication stream, events[2] on `stream` after the interior rows (split 1) or
+ * once the halos are in (split 0: after `stream`'s wait for them, before the launch),
+ * events[3] after the last filter launch on `stream`. */
 int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream,
                         void* const* events);
 
@@ -130,6 +131,28 @@ int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t o
  * on `stream`. Every rank must batch the same frames in the same order. */
 int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* const* d_outs, size_t out_pitch,
                         void* stream);
+
+/* Graph mode (0 default, 1 on): vip_shard_run captures a frame's whole sequence -- own
+ * rows written, the RCCL group on the communication stream, the filter launches -- once per
+ * (d_slab, d_out, out_pitch, stream) into a hipGraph and replays it with one hipGraphLaunch
+ * (host cost a few us instead of an RCCL group's 16-30 us). The first run of a shard is
+ * always direct (RCCL connects its peers lazily, which a capture cannot do), as is any run
+ * on the null stream. A shard's communicator must serve one stream at a time: frames in
+ * flight on several streams take one shard each. Up to 64 graphs are kept per shard; a
+ * change of split or vip_shard_set_graph(h, 0) drops them. */
+int vip_shard_set_graph(vip_shard_t h, int on);
+
+/* Number of graphs a shard holds (graph mode). */
+int vip_shard_graph_count(vip_shard_t h, int* count);
+
+/* Test transport, one GPU: shard `rank` of an nranks-way geometry whose row neighbours are
+ * the shard ITSELF over a one-rank RCCL communicator. The halo above receives the shard's
+ * own top halo_rows rows and the halo below its own bottom rows, through the same
+ * ncclSend/ncclRecv group, events, split, batch and graph code as a multi-process run, so
+ * the result equals the filter of the slab taken as a frame of its own, on its own rows.
+ * kind VIP_FILTER_BILATERAL / _ADAPTIVE (sigmas) or VIP_FILTER_TEXTURE (nitr). */
+int vip_shard_create_loopback(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
+                              float sigma_color, int nitr, int numerics, int nranks, int rank, int timeout_ms);
 
 /* One filter application of every shard of a group created by vip_shard_create_group
  * (one process): slabs[i], outs[i] (pitch out_pitch) and streams[i] on shard i's device. */

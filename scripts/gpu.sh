@@ -1,0 +1,92 @@
+#!/bin/bash
+# The one parametrised GPU runner (round 4 on; it replaces the per-round gpu_r0x_*.sh
+# wrappers). Run through gpurun from the repo root:
+#
+#   TAG=r04 bash scripts/gpu.sh STEP [STEP ...]
+#
+# Every step runs under its own time limit; the first failing step ends the run, and no
+# GPU step follows a fault, abort or timeout. Outputs go to gpurun_out/ (copy what is to
+# be judged into profiles/).
+#
+# STEP
+#   tests[=ARGS]        python -m pytest -m gpu ARGS (default: tests, the whole GPU suite)
+#   smoke               __graft_entry__.smoke()
+#   bench=CFG[,A,..]    bench line              -> ${TAG}_CFG_bench.json (A: extra bench.py args)
+#   stats=CFG[,A,..]    rocprofv3 --kernel-trace --stats of a short bench run
+#                                               -> ${TAG}_CFG_kernel_stats.csv, ${TAG}_CFG_busy.json
+#   pmc=CFG[,A,..]      one rocprofv3 --pmc pass per counter set -> ${TAG}_CFG_pmc.json
+#   rehearse=CFG,N      the N > 1 native path on one GPU: bench.py --rehearse-native --loopback N
+#                                               -> ${TAG}_CFG_loopbackN.json
+#   gloo=CFG,N          python bench.py --gpus N --same-device --backend gloo (N ranks on cuda:0)
+#                                               -> ${TAG}_CFG_gloo{N}.json
+#   py=SCRIPT[,A,..]    python SCRIPT A..       -> ${TAG}_<script name>.txt
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+TAG=${TAG:-r04}
+O=gpurun_out
+
+fail() { echo "step '$1' failed rc=$2"; [ -n "${3:-}" ] && tail -25 "$3"; exit "$2"; }
+
+# counter sets, one rocprofv3 pass each (at most 8 SQ_, 4 TCC_ per pass)
+PMC_SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+          "SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+          "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU GRBM_GUI_ACTIVE"
+          "FETCH_SIZE" "WRITE_SIZE")
+
+for step in "$@"; do
+  name=${step%%=*}
+  arg=""; [ "$step" != "$name" ] && arg=${step#*=}
+  IFS=, read -r -a A <<< "$arg"
+  echo "== $step"
+  case $name in
+    tests)
+      log=$O/${TAG}_pytest_gpu.log
+      timeout -k 10 1100 python -u -m pytest ${arg:-tests} -m gpu -v -x -rf --durations=15 --timeout 300 \
+        --timeout-method thread > $log 2>&1
+      rc=$?; tail -8 $log; [ $rc -eq 0 ] || fail "$step" $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1
+      rc=$?; tail -2 $O/${TAG}_smoke.log; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_smoke.log ;;
+    bench)
+      cfg=${A[0]}; out=$O/${TAG}_${cfg}_bench.json
+      timeout -k 10 400 python bench.py --config $cfg "${A[@]:1}" > $out 2> $O/${TAG}_${cfg}_bench.err
+      rc=$?; cut -c1-600 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_bench.err ;;
+    stats)
+      cfg=${A[0]}; steps=20; [ $cfg = c5 ] && steps=5; d=$O/prof_${TAG}_$cfg
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
+        python bench.py --config $cfg --steps $steps --warmup 3 --no-cpu-baseline "${A[@]:1}" > $d.log 2>&1
+      rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
+      cp $d/run_kernel_stats.csv $O/${TAG}_${cfg}_kernel_stats.csv
+      python scripts/kernel_busy.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_busy.json > /dev/null || fail "$step" $?
+      head -4 $O/${TAG}_${cfg}_kernel_stats.csv | cut -c1-200 ;;
+    pmc)
+      cfg=${A[0]}; d=$O/pmc_${TAG}_$cfg; mkdir -p $d; i=0
+      for set in "${PMC_SETS[@]}"; do
+        i=$((i+1))
+        timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $set -d $d/p$i -o run --output-format csv -- \
+          python bench.py --config $cfg --streams 1 --steps 5 --warmup 1 --settle-s 0.3 --no-cpu-baseline \
+          "${A[@]:1}" > $d/p$i.log 2>&1
+        rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || fail "$step pass $i" $rc $d/p$i.log
+      done
+      python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json | cut -c1-400 || fail "$step" $? ;;
+    rehearse)
+      cfg=${A[0]}; n=${A[1]}; out=$O/${TAG}_${cfg}_loopback$n.json
+      timeout -k 10 400 python bench.py --config $cfg --rehearse-native --loopback $n --steps ${A[2]:-400} \
+        > $out 2> $O/${TAG}_${cfg}_loopback$n.err
+      rc=$?; cut -c1-1500 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_loopback$n.err ;;
+    gloo)
+      cfg=${A[0]}; n=${A[1]}; out=$O/${TAG}_${cfg}_gloo$n.json
+      timeout -k 10 500 python bench.py --gpus $n --same-device --backend gloo --config $cfg --steps ${A[2]:-8} \
+        --warmup 1 > $out 2> $O/${TAG}_${cfg}_gloo$n.err
+      rc=$?; cut -c1-800 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_gloo$n.err ;;
+    py)
+      s=${A[0]}; out=$O/${TAG}_$(basename ${s%.*}).txt
+      timeout -k 10 600 python $s "${A[@]:1}" > $out 2>&1
+      rc=$?; tail -30 $out; [ $rc -eq 0 ] || fail "$step" $rc ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "gpu.sh: all steps done"

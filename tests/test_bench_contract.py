@@ -92,3 +92,68 @@ def test_halo_batches_keep_buffers_on_one_stream():
                 st = (i // B) % S
                 assert seen.setdefault(i % bench.NBUF, st) == st
     assert bench.halo_batches(2) == [1, 2, 3]
+
+
+# --- `python bench.py --gpus N` starts its own N ranks -------------
+PROBE = r'''
+import json, os, sys, time
+rank = os.environ["RANK"]
+with open(os.path.join(sys.argv[1], f"rank{rank}.json"), "w") as fh:
+    json.dump({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                                              "HSA_ENABLE_IPC_MODE_LEGACY")} | {"argv": sys.argv[1:]}, fh)
+if sys.argv[2] == "sleep":
+    time.sleep(120)
+sys.exit(int(sys.argv[2]) if rank == "1" and sys.argv[2] != "sleep" else 0)
+'''
+
+
+def test_rank_launch_argv_is_the_drivers_form():
+    cmd = bench.rank_launch_argv(4, ["--gpus", "4", "--config", "c5"], 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=4" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29555" in cmd
+    assert cmd[-5:] == [os.path.join(ROOT, "bench.py"), "--gpus", "4", "--config", "c5"]
+
+
+def _probe(tmp_path):
+    script = tmp_path / "probe.py"
+    script.write_text(PROBE)
+    return str(script)
+
+
+def test_launch_ranks_env_and_status(tmp_path):
+    script = _probe(tmp_path)
+    rc = bench.launch_ranks(2, [str(tmp_path), "0"], timeout_s=120, script=script)
+    assert rc == 0
+    envs = [json.loads((tmp_path / f"rank{r}.json").read_text()) for r in (0, 1)]
+    for r, e in enumerate(envs):
+        assert e["RANK"] == str(r) and e["LOCAL_RANK"] == str(r) and e["WORLD_SIZE"] == "2"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and int(e["MASTER_PORT"]) > 0
+        assert e["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+        assert e["argv"] == [str(tmp_path), "0"]
+    # one failing rank fails the run
+    assert bench.launch_ranks(2, [str(tmp_path), "3"], timeout_s=120, script=script) != 0
+
+
+def test_launch_ranks_timeout_ends_every_rank(tmp_path):
+    import time
+    script = _probe(tmp_path)
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(2, [str(tmp_path), "sleep"], timeout_s=15, script=script)
+    assert rc == 124 and time.monotonic() - t0 < 60
+    # the ranks were started (they wrote their env) and are gone now
+    assert (tmp_path / "rank0.json").exists() and (tmp_path / "rank1.json").exists()
+
+
+def test_bench_gpus_2_from_a_plain_shell_launches_ranks():
+    """`python bench.py --gpus 2` without WORLD_SIZE starts two ranks through torchrun; on
+    this GPU-less host they fail, and that failure is the command's status (no exit at the
+    launch check, no hang)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--launch-timeout", "240"], capture_output=True, text=True, env=env, timeout=300)
+    assert "starting 2 ranks" in r.stderr
+    assert "torch.distributed.run" in r.stderr
+    assert r.returncode not in (0, 124)

@@ -19,7 +19,7 @@ import pytest
 
 import various_image_processings_amd as vip
 from various_image_processings_amd import _shard_lib as S
-from various_image_processings_amd.sharded import NativeShard, ShardGroup, native_unique_id
+from various_image_processings_amd.sharded import NativeShard, ShardGroup, native_unique_id, texture_halo_rows
 
 pytestmark = pytest.mark.gpu
 
@@ -227,3 +227,160 @@ def test_shard_frame_sample(dev, argv):
     assert os.path.exists(exe), "build first"
     r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "equals the one-launch output" in r.stdout, r.stdout + r.stderr[-2000:]
+
+
+# --- loopback transport: the RCCL neighbour path on one GPU --------------------------
+# vip_shard_create_loopback: the shard's row neighbours are itself over a one-rank
+# communicator, so enqueue_p2p's ncclSend/ncclRecv pairs, the group end, the ev_in / ev_x
+# ordering, the batch group and graph capture all run for real. The halo above receives
+# the shard's own top r rows and the halo below its own bottom r rows, so the expected
+# output is the filter of that slab taken as a frame, on the own rows.
+def _loopback_frame(img, r, rank, n):
+    parts = [img[:r]] if rank > 0 else []
+    parts.append(img)
+    if rank < n - 1:
+        parts.append(img[-r:])
+    return np.ascontiguousarray(np.concatenate(parts)), (r if rank > 0 else 0)
+
+
+def _loopback_slab(dev, s, img):
+    geo = s.geo
+    slab = dev.empty((geo.slab_rows, img.shape[1], 3))
+    slab.fill_(201)  # the exchange overwrites the halos it owns
+    slab[geo.radius:geo.radius + geo.own] = dev.put(img)
+    return slab
+
+
+def _loopback_want(dev, img, k, rank, n, adaptive=False, nitr=None):
+    r = k // 2 if nitr is None else nitr * texture_halo_rows(k)
+    frame, top = _loopback_frame(img, r, rank, n)
+    return _single(dev, frame, k, adaptive, nitr)[top:top + img.shape[0]]
+
+
+@pytest.mark.parametrize("rank", [0, 1, 2])
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_loopback_rccl_exchange(dev, oracle, rank, adaptive):
+    torch = dev.torch_
+    w, own = 1000, 300
+    img = oracle.random_image(w, own)
+    s = NativeShard(w, 3 * own, 15, rank, 3, None, adaptive=adaptive, loopback=True)
+    assert s.geo.own == own
+    want = _loopback_want(dev, img, 15, rank, 3, adaptive)
+    for split in (True, False, True):
+        s.set_split(split)
+        slab = _loopback_slab(dev, s, img)
+        out = dev.empty((own, w, 3))
+        s.filter(slab, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(dev.get(out), want), split
+
+
+def test_loopback_against_the_oracle(dev, oracle):
+    w, own = 131, 40
+    img = oracle.random_u8(w * own * 3).reshape(own, w, 3)
+    s = NativeShard(w, 3 * own, 9, 1, 3, None, loopback=True)
+    s.set_split(True)
+    slab = _loopback_slab(dev, s, img)
+    out = dev.empty((own, w, 3))
+    s.filter(slab, out)
+    dev.torch_.cuda.synchronize()
+    frame, top = _loopback_frame(img, 4, 1, 3)
+    assert np.array_equal(dev.get(out), oracle.bilateral(frame, 9)[top:top + own])
+
+
+def test_loopback_timed_events_in_order(dev, oracle):
+    """split 0: events[2] is recorded once the filter stream has the halos (after the wait),
+    so it is not earlier than the exchange's end (events[1]); split 1: after the interior."""
+    torch = dev.torch_
+    w, own = 3840, 270
+    img = oracle.random_image(w, own)
+    s = NativeShard(w, 8 * own, 15, 3, 8, None, loopback=True)
+    want = _loopback_want(dev, img, 15, 3, 8)
+    slab = _loopback_slab(dev, s, img)
+    out = dev.empty((own, w, 3))
+    s.filter(slab, out)  # the first exchange connects the peer
+    for split in (False, True):
+        s.set_split(split)
+        for _ in range(3):
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            out.zero_()
+            s.filter_timed(slab, out, ev)
+            torch.cuda.synchronize()
+            assert np.array_equal(dev.get(out), want)
+            t1, t2, t3 = (ev[0].elapsed_time(ev[j]) for j in (1, 2, 3))
+            assert 0 <= t2 <= t3 and t1 <= t3
+            if not split:
+                assert t1 <= t2 + 1e-3
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_loopback_batch(dev, oracle, split):
+    """vip_shard_run_batch with neighbours: the halos of three frames in one RCCL group."""
+    torch = dev.torch_
+    w, own = 900, 200
+    imgs = [oracle.random_image(w, own), np.ascontiguousarray(oracle.random_image(w, own)[::-1])]
+    imgs.append(np.ascontiguousarray(imgs[0][:, ::-1]))
+    s = NativeShard(w, 4 * own, 15, 2, 4, None, loopback=True)
+    s.set_split(split)
+    slabs = [_loopback_slab(dev, s, im) for im in imgs]
+    outs = [dev.empty((own, w, 3)) for _ in imgs]
+    s.batch_launcher()([t.data_ptr() for t in slabs], [t.data_ptr() for t in outs],
+                       torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for im, o in zip(imgs, outs):
+        assert np.array_equal(dev.get(o), _loopback_want(dev, im, 15, 2, 4))
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_loopback_graph_replay_two_streams(dev, oracle, split):
+    """Graph mode with one shard (own communicator) per stream and two frames in flight:
+    every replayed frame equals its direct run; one graph per (slab, out, stream)."""
+    torch = dev.torch_
+    w, own, n = 3840, 270, 8
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    shards = [NativeShard(w, n * own, 15, 5, n, None, loopback=True) for _ in streams]
+    imgs = [oracle.random_image(w, own)] + [np.ascontiguousarray(np.roll(oracle.random_image(w, own), 7 * i, axis=1))
+                                            for i in range(1, 6)]
+    wants = [_loopback_want(dev, im, 15, 5, n) for im in imgs]
+    slabs = [_loopback_slab(dev, shards[0], im) for im in imgs]
+    outs = [dev.empty((own, w, 3)) for _ in imgs]
+    for x in shards:
+        x.set_split(split)
+        x.set_graph(True)
+    launch = [x.launcher() for x in shards]
+    torch.cuda.synchronize()
+    for rnd in range(4):  # round 0 runs direct (connects the peer), round 1 captures, then replays
+        for o in outs:
+            o.fill_(3)
+        torch.cuda.synchronize()
+        for i in range(len(imgs)):  # buffer i always on stream i % 2 (and its shard)
+            h = i % 2
+            launch[h](slabs[i].data_ptr(), outs[i].data_ptr(), streams[h].cuda_stream)
+        torch.cuda.synchronize()
+        for i, o in enumerate(outs):
+            assert np.array_equal(dev.get(o), wants[i]), (rnd, i)
+    assert [x.graph_count() for x in shards] == [3, 3]
+    shards[0].set_graph(False)
+    assert shards[0].graph_count() == 0
+
+
+def test_loopback_texture_graph(dev, oracle):
+    """The texture shard (45-row halo at k = 5, nitr = 5) through the loopback exchange,
+    direct and replayed from a graph."""
+    torch = dev.torch_
+    w, own = 1200, 300
+    img = oracle.random_image(w, own)
+    s = NativeShard(w, 3 * own, 5, 1, 3, None, nitr=5, loopback=True)
+    want = _loopback_want(dev, img, 5, 1, 3, nitr=5)
+    slab = _loopback_slab(dev, s, img)
+    out = dev.empty((own, w, 3))
+    st = torch.cuda.Stream()
+    s.set_graph(True)
+    run = s.launcher()
+    for _ in range(3):
+        out.zero_()
+        torch.cuda.synchronize()
+        run(slab.data_ptr(), out.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(dev.get(out), want)
+    assert s.graph_count() == 1

@@ -112,7 +112,19 @@ struct vip_shard_s {
     hipEvent_t ev_in = nullptr;  // own rows written (on the caller's stream)
     hipEvent_t ev_x = nullptr;   // halos received (on comm)
     ncclComm_t nccl = nullptr;   // VIP_SHARD_RCCL
+    int peer_up = -1, peer_down = -1;  // communicator ranks of the row neighbours (loopback: 0, itself)
     int split = 0;               // 1: interior rows under the exchange, then the edge bands
+    // graph mode (vip_shard_set_graph): one captured hipGraph per (slab, out, pitch, stream)
+    struct Graph {
+        uint8_t* slab;
+        uint8_t* out;
+        size_t pitch;
+        hipStream_t stream;
+        hipGraphExec_t exec;
+    };
+    int graph = 0;
+    bool warm = false;           // one direct exchange done: RCCL connects peers lazily, a capture cannot
+    std::vector<Graph> graphs;
     bool above() const { return rank > 0 && r > 0; }
     bool below() const { return rank < nranks - 1 && r > 0; }
     int slab_rows() const { return own + 2 * r; }
@@ -191,6 +203,8 @@ int new_shard(vip_shard_s** out, const FilterSpec& f, int width, int frame_heigh
     h->timeout_ms = default_timeout(timeout_ms);
     vip_shard_rows(frame_height, nranks, rank, &h->row_begin, &h->own);
     h->r = r;
+    h->peer_up = rank - 1;
+    h->peer_down = rank + 1;
     *out = h;
     return 0;
 }
@@ -254,14 +268,15 @@ int enqueue_p2p(const vip_shard_s* h, uint8_t* slab) {
     const size_t bytes = (size_t)h->r * h->pitch();
     ncclResult_t e = ncclSuccess;
     if (h->above()) {
-        if ((e = ncclSend(slab + (size_t)h->r * h->pitch(), bytes, ncclUint8, h->rank - 1, h->nccl, h->comm)))
+        if ((e = ncclSend(slab + (size_t)h->r * h->pitch(), bytes, ncclUint8, h->peer_up, h->nccl, h->comm)))
             return comm_fail(e, "ncclSend (up)");
-        if ((e = ncclRecv(slab, bytes, ncclUint8, h->rank - 1, h->nccl, h->comm))) return comm_fail(e, "ncclRecv (up)");
+        if ((e = ncclRecv(slab, bytes, ncclUint8, h->peer_up, h->nccl, h->comm))) return comm_fail(e, "ncclRecv (up)");
     }
     if (h->below()) {
-        if ((e = ncclSend(slab + (size_t)h->own * h->pitch(), bytes, ncclUint8, h->rank + 1, h->nccl, h->comm)))
+        if ((e = ncclSend(slab + (size_t)h->own * h->pitch(), bytes, ncclUint8, h->peer_down, h->nccl, h->comm)))
             return comm_fail(e, "ncclSend (down)");
-        if ((e = ncclRecv(slab + (size_t)(h->r + h->own) * h->pitch(), bytes, ncclUint8, h->rank + 1, h->nccl, h->comm)))
+        if ((e = ncclRecv(slab + (size_t)(h->r + h->own) * h->pitch(), bytes, ncclUint8, h->peer_down, h->nccl,
+                          h->comm)))
             return comm_fail(e, "ncclRecv (down)");
     }
     return 0;
@@ -289,6 +304,16 @@ struct DeviceGuard {  // restores the caller's current device
     }
 };
 
+void free_graphs(vip_shard_s* h) {
+    for (auto& g : h->graphs) {
+        (void)hipStreamSynchronize(g.stream);  // a replay may still be in flight
+        (void)hipGraphExecDestroy(g.exec);
+    }
+    h->graphs.clear();
+}
+
+constexpr size_t kMaxGraphs = 64;  // captured (slab, out, stream) combinations kept per shard
+
 }  // namespace
 
 extern "C" {
@@ -313,6 +338,28 @@ int vip_shard_unique_id(void* id) {
 
 const char* vip_shard_last_error(void) { return g_last_error.c_str(); }
 
+// This shard's communicator: rank comm_rank of comm_n over the id (bounded, see InitJob).
+static int init_comm(vip_shard_s* h, const ncclUniqueId& u, int comm_n, int comm_rank) {
+    const int dev = h->device;
+    auto job = std::make_shared<InitJob>();
+    std::vector<ncclComm_t> comms;
+    const int rc = bounded_init(
+        job,
+        [u, comm_n, comm_rank, dev](InitJob& j) {
+            j.comms.assign(1, nullptr);
+            if (hipSetDevice(dev) != hipSuccess) return (int)hipErrorInvalidDevice;
+            const ncclResult_t e = ncclCommInitRank(&j.comms[0], comm_n, u, comm_rank);
+            if (e != ncclSuccess) {
+                j.error = std::string("ncclCommInitRank: ") + ncclGetErrorString(e);
+                return (int)VIP_ERR_COMM;
+            }
+            return 0;
+        },
+        h->timeout_ms, &comms);
+    if (!rc) h->nccl = comms[0];
+    return rc;
+}
+
 static int create_rank(vip_shard_t* out, const FilterSpec& f, int width, int frame_height, int nranks, int rank,
                        const void* id, int timeout_ms) {
     if (!out || !id) return VIP_ERR_INVALID_ARGUMENT;
@@ -323,23 +370,7 @@ static int create_rank(vip_shard_t* out, const FilterSpec& f, int width, int fra
     if (!rc) {
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        const int dev = h->device;
-        auto job = std::make_shared<InitJob>();
-        std::vector<ncclComm_t> comms;
-        rc = bounded_init(
-            job,
-            [u, nranks, rank, dev](InitJob& j) {
-                j.comms.assign(1, nullptr);
-                if (hipSetDevice(dev) != hipSuccess) return (int)hipErrorInvalidDevice;
-                const ncclResult_t e = ncclCommInitRank(&j.comms[0], nranks, u, rank);
-                if (e != ncclSuccess) {
-                    j.error = std::string("ncclCommInitRank: ") + ncclGetErrorString(e);
-                    return (int)VIP_ERR_COMM;
-                }
-                return 0;
-            },
-            h->timeout_ms, &comms);
-        if (!rc) h->nccl = comms[0];
+        rc = init_comm(h, u, nranks, rank);
     }
     if (rc) {
         vip_shard_destroy(h);
@@ -425,10 +456,57 @@ int vip_shard_create_group_texture(vip_shard_t* out, int n, int transport, const
                         width, frame_height, timeout_ms);
 }
 
+int vip_shard_create_loopback(vip_shard_t* out, int kind, int width, int frame_height, int ksize, float sigma_space,
+                              float sigma_color, int nitr, int numerics, int nranks, int rank, int timeout_ms) {
+    if (!out) return VIP_ERR_INVALID_ARGUMENT;
+    if (kind != VIP_FILTER_BILATERAL && kind != VIP_FILTER_ADAPTIVE && kind != VIP_FILTER_TEXTURE)
+        return VIP_ERR_INVALID_ARGUMENT;
+    const FilterSpec f{kind, ksize, sigma_space, sigma_color, kind == VIP_FILTER_TEXTURE ? nitr : 0, numerics};
+    vip_shard_s* h = nullptr;
+    int rc = new_shard(&h, f, width, frame_height, nranks, rank, VIP_SHARD_RCCL, timeout_ms);
+    if (rc) return rc;
+    rc = init_shard(h, f);
+    if (!rc) {
+        ncclUniqueId u;
+        if (const ncclResult_t e = ncclGetUniqueId(&u)) rc = comm_fail(e, "ncclGetUniqueId");
+        if (!rc) rc = init_comm(h, u, 1, 0);
+    }
+    if (rc) {
+        vip_shard_destroy(h);
+        return rc;
+    }
+    h->peer_up = h->peer_down = 0;  // both neighbours are this rank of the one-rank communicator
+    *out = h;
+    return 0;
+}
+
 int vip_shard_set_split(vip_shard_t h, int split) {
     if (!h || (split != 0 && split != 1)) return VIP_ERR_INVALID_ARGUMENT;
     if (split && h->kind == VIP_FILTER_TEXTURE) return VIP_ERR_INVALID_ARGUMENT;  // every iteration needs the halos
+    if (split != h->split) {
+        DeviceGuard guard;
+        (void)hipSetDevice(h->device);
+        free_graphs(h);  // the captured sequences follow the old split
+    }
     h->split = split;
+    return 0;
+}
+
+int vip_shard_set_graph(vip_shard_t h, int on) {
+    if (!h || (on != 0 && on != 1)) return VIP_ERR_INVALID_ARGUMENT;
+    if (h->transport != VIP_SHARD_RCCL) return VIP_ERR_INVALID_ARGUMENT;
+    if (!on) {
+        DeviceGuard guard;
+        (void)hipSetDevice(h->device);
+        free_graphs(h);
+    }
+    h->graph = on;
+    return 0;
+}
+
+int vip_shard_graph_count(vip_shard_t h, int* count) {
+    if (!h || !count) return VIP_ERR_INVALID_ARGUMENT;
+    *count = (int)h->graphs.size();
     return 0;
 }
 
@@ -440,12 +518,15 @@ int vip_shard_geometry(vip_shard_t h, int* row_begin, int* own_rows, int* halo_r
     return 0;
 }
 
-static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitch, void* stream,
-                     void* const* events) {
+static int check_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitch) {
     if (!h || !slab || !out || out_pitch < h->pitch() || h->transport != VIP_SHARD_RCCL || !h->nccl)
         return VIP_ERR_INVALID_ARGUMENT;
-    const hipStream_t s = (hipStream_t)stream;
-    VIP_HIP_TRY(hipSetDevice(h->device));
+    return 0;
+}
+
+// One frame's work enqueued on `s` (and the communication stream), device already set.
+static int enqueue_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitch, hipStream_t s,
+                       void* const* events) {
     int rc = mark(events, 0, s);
     if (!rc && !h->above() && !h->below()) {  // no neighbours: one launch over the own rows
         rc = mark(events, 1, s);
@@ -468,8 +549,8 @@ static int shard_run(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
     if (!rc) rc = mark(events, 1, h->comm);
     if (!rc) rc = (int)hipEventRecord(h->ev_x, h->comm);
     if (!h->split) {  // one launch over the own rows once the halos are in
-        if (!rc) rc = mark(events, 2, s);
         if (!rc) rc = (int)hipStreamWaitEvent(s, h->ev_x, 0);
+        if (!rc) rc = mark(events, 2, s);  // halos in, on the filter stream
         if (!rc) rc = filter_rows(h, slab, out, out_pitch, 0, h->own, s);
         if (!rc) rc = mark(events, 3, s);
         return rc;
@@ -504,6 +585,7 @@ int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* 
     for (int f = 0; f < n && !rc; ++f) rc = enqueue_p2p(h, d_slabs[f]);
     const int rc2 = group_end(&h, 1);
     if (rc || rc2) return rc ? rc : rc2;
+    h->warm = true;
     VIP_HIP_TRY(hipEventRecord(h->ev_x, h->comm));
     if (!h->split) {
         VIP_HIP_TRY(hipStreamWaitEvent(s, h->ev_x, 0));
@@ -519,16 +601,62 @@ int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* 
     return 0;
 }
 
+// Graph mode: the frame's whole sequence (own rows written -> exchange on the
+// communication stream -> filter launches) captured once per (slab, out, pitch, stream)
+// into a hipGraph and replayed with one hipGraphLaunch: a few us of host time per frame
+// instead of an RCCL group's 16-30 us (profiles/r03_rccl_enqueue.txt). Each shard has its
+// own communicator, so the graphs of shards on different streams never run one
+// communicator's kernels concurrently.
+static int run_graph(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitch, hipStream_t s) {
+    for (const auto& g : h->graphs)
+        if (g.slab == slab && g.out == out && g.pitch == out_pitch && g.stream == s)
+            return (int)hipGraphLaunch(g.exec, s);
+    if (h->graphs.size() >= kMaxGraphs) {
+        VIP_HIP_TRY(hipStreamSynchronize(s));  // the oldest graph may still be in flight on s
+        (void)hipGraphExecDestroy(h->graphs.front().exec);
+        h->graphs.erase(h->graphs.begin());
+    }
+    // nothing is enqueued yet: if the stream cannot capture, run this frame directly
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        return enqueue_run(h, slab, out, out_pitch, s, nullptr);
+    }
+    const int rc = enqueue_run(h, slab, out, out_pitch, s, nullptr);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &graph);
+    if (rc || e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return rc ? rc : (int)e;
+    }
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) return (int)ei;
+    h->graphs.push_back({slab, out, out_pitch, s, exec});
+    return (int)hipGraphLaunch(exec, s);
+}
+
 int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream) {
+    if (const int rc = check_run(h, d_slab, d_out, out_pitch)) return rc;
     DeviceGuard guard;
-    return shard_run(h, d_slab, d_out, out_pitch, stream, nullptr);
+    VIP_HIP_TRY(hipSetDevice(h->device));
+    const hipStream_t s = (hipStream_t)stream;
+    // the null stream cannot be captured; the first exchange connects the peers directly
+    if (h->graph && h->warm && s != nullptr) return run_graph(h, d_slab, d_out, out_pitch, s);
+    const int rc = enqueue_run(h, d_slab, d_out, out_pitch, s, nullptr);
+    if (!rc) h->warm = true;
+    return rc;
 }
 
 int vip_shard_run_timed(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream,
                         void* const* events) {
     if (!events) return VIP_ERR_INVALID_ARGUMENT;
+    if (const int rc = check_run(h, d_slab, d_out, out_pitch)) return rc;
     DeviceGuard guard;
-    return shard_run(h, d_slab, d_out, out_pitch, stream, events);
+    VIP_HIP_TRY(hipSetDevice(h->device));
+    const int rc = enqueue_run(h, d_slab, d_out, out_pitch, (hipStream_t)stream, events);
+    if (!rc) h->warm = true;
+    return rc;
 }
 
 int vip_shard_run_group(vip_shard_t* hs, int n, uint8_t* const* slabs, uint8_t* const* outs, size_t out_pitch,
@@ -605,6 +733,7 @@ int vip_shard_destroy(vip_shard_t h) {
     if (!h) return 0;
     DeviceGuard guard;
     (void)hipSetDevice(h->device);
+    free_graphs(h);
     if (h->nccl) {  // only complete communicators are stored (bounded_init)
         ncclResult_t st = ncclSuccess;
         if (ncclCommGetAsyncError(h->nccl, &st) == ncclSuccess && st == ncclSuccess)

@@ -314,15 +314,24 @@ def _native_halo(ksize: int, nitr) -> int:
 
 class NativeShard:
     """This rank's shard of a row-sharded frame (one process per GPU, RCCL transport).
-    nitr given: the bilateral texture filter (vip_shard_create_texture; ksize is its k)."""
+    nitr given: the bilateral texture filter (vip_shard_create_texture; ksize is its k).
+    loopback=True (unique_id ignored): vip_shard_create_loopback, the test transport whose
+    row neighbours are this shard itself over a one-rank communicator (one GPU)."""
 
     def __init__(self, width: int, frame_height: int, ksize: int, rank: int, world: int, unique_id: bytes,
                  sigma_space: float = 10.0, sigma_color: float = 30.0, adaptive: bool = False, numerics: int = 0,
-                 timeout_ms: int = 180000, nitr=None):
+                 timeout_ms: int = 180000, nitr=None, loopback: bool = False):
         import ctypes
+        from . import _lib
         from . import _shard_lib as S
         self._h = ctypes.c_void_p()
-        idb = ctypes.create_string_buffer(bytes(unique_id), S.VIP_SHARD_ID_BYTES)
+        if loopback:
+            kind = _lib.VIP_FILTER_TEXTURE if nitr is not None else _shard_kind(adaptive)
+            S.call("vip_shard_create_loopback", ctypes.byref(self._h), kind, width, frame_height, ksize, sigma_space,
+                   sigma_color, nitr or 0, numerics, world, rank, int(timeout_ms))
+            self.geo = SlabGeometry(width, frame_height, _native_halo(ksize, nitr), rank, world)
+            return
+        idb = ctypes.create_string_buffer(bytes(unique_id or b""), S.VIP_SHARD_ID_BYTES)
         if nitr is None:
             S.call("vip_shard_create", ctypes.byref(self._h), _shard_kind(adaptive), width, frame_height, ksize,
                    sigma_space, sigma_color, numerics, world, rank, idb, int(timeout_ms))
@@ -336,6 +345,18 @@ class NativeShard:
         (True), or one launch after the exchange (False, the default)."""
         from . import _shard_lib as S
         S.call("vip_shard_set_split", self._h, 1 if split else 0)
+
+    def set_graph(self, on: bool) -> None:
+        """vip_shard_set_graph: replay one captured hipGraph per (slab, out, stream)."""
+        from . import _shard_lib as S
+        S.call("vip_shard_set_graph", self._h, 1 if on else 0)
+
+    def graph_count(self) -> int:
+        import ctypes
+        from . import _shard_lib as S
+        n = ctypes.c_int()
+        S.call("vip_shard_graph_count", self._h, ctypes.byref(n))
+        return n.value
 
     def filter(self, slab, out, stream=None) -> None:
         """slab: (own + 2r, W, 3) uint8 with own rows filled; out: (own, W, 3). Asynchronous."""
