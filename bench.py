@@ -295,56 +295,70 @@ def cpu_baseline(cfg) -> dict:
                        f"include/cpp numerics, all k*k taps like the reference loop)")
 
 
-def pmc_traffic(config: str, kernels: list, per_step: int = 1):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this config
-    (profiles/r*_<config>_pmc.json, written by scripts/pmc_summary.py from
-    scripts/gpu_pmc.sh: FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE).
-    Returns (bytes, source) or (None, None) when no summary matches the kernels."""
+def pmc_summary(config: str, kernel, need: str):
+    """(entry, source) from the newest committed rocprofv3 PMC summary of this config
+    (profiles/r*_<config>_pmc.json, written by scripts/pmc_summary.py) that holds EXACTLY
+    this kernel -- its full template signature, as vip_launched_kernels names the kernel
+    the line timed -- with the field `need` ("traffic_bytes", or a counter name); (None,
+    None) otherwise. A summary of another instantiation (another tiling, or an older
+    build's template list) is stale for this line and is never used."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
-    if not files:
+    if not kernel:
         return None, None
-    with open(files[-1]) as fh:
-        ks = json.load(fh)["kernels"]
-    total = 0.0
-    for want in kernels:
-        hit = [v for n, v in ks.items() if n.startswith(want) and "traffic_bytes" in v]
-        if not hit:
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")), reverse=True):
+        with open(f) as fh:
+            e = json.load(fh)["kernels"].get(kernel)
+        if e and (need in e or need in e.get("counters", {})):
+            return e, os.path.relpath(f, ROOT)
+    return None, None
+
+
+def pmc_traffic(config: str, kernels: list, per_step: int = 1):
+    """HBM bytes per launch of these exact kernels from the committed PMC summaries
+    (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, scripts/pmc_summary.py).
+    Returns (bytes, source) or (None, None) when any kernel has no exact summary."""
+    total, srcs = 0.0, []
+    for k in kernels:
+        e, src = pmc_summary(config, k, "traffic_bytes")
+        if e is None:
             return None, None
-        total += hit[0]["traffic_bytes"]
-    return total * per_step, os.path.relpath(files[-1], ROOT)
+        total += e["traffic_bytes"]
+        srcs.append(src)
+    return total * per_step, ", ".join(sorted(set(srcs)))
 
 
-def valu_issue(config: str, kernel: str, launch_ms: float):
+def launched(kernels: list, prefix: str):
+    """The launched kernel (exact name) that starts with prefix, or None."""
+    hit = [k for k in kernels if k.startswith(prefix)]
+    return hit[0] if hit else None
+
+
+def valu_issue(config: str, kernel, launch_ms: float):
     """VALU-issue roofline of one kernel: its SQ_INSTS_VALU wave-instructions per launch
-    (committed PMC summary) / the live event-timed launch, against 1024 SIMDs issuing one
-    wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md) at the 2.4 GHz maximum
-    clock and at the clock the chip held under this load (GRBM_GUI_ACTIVE / 8 XCDs /
-    launch time). None when no summary matches."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_pmc.json")))
-    if not files:
+    (committed PMC summary of exactly this kernel) / the live event-timed launch, against
+    1024 SIMDs issuing one wave64 VALU instruction per 2 cycles (MI355X_MICROARCH.md) at
+    the 2.4 GHz maximum clock and at the clock the chip held under this load
+    (GRBM_GUI_ACTIVE / 8 XCDs / launch time). None when no summary matches."""
+    e, src = pmc_summary(config, kernel, "SQ_INSTS_VALU")
+    if e is None:
         return None
-    with open(files[-1]) as fh:
-        ks = json.load(fh)["kernels"]
-    hit = [v["counters"] for n, v in ks.items() if n.startswith(kernel) and "SQ_INSTS_VALU" in v.get("counters", {})]
-    if not hit:
-        return None
-    c = hit[0]
+    c = e["counters"]
     achieved = c["SQ_INSTS_VALU"] / (launch_ms * 1e-3) / 1e9
     peak = VALU_SIMDS * 2.4 / VALU_CYCLES_PER_INSTR
     out = dict(achieved=round(achieved, 1), peak=round(peak, 1), unit="G wave-instr/s",
-               frac=round(achieved / peak, 4), wave_instr_per_launch=c["SQ_INSTS_VALU"],
-               source=os.path.relpath(files[-1], ROOT))
+               frac=round(achieved / peak, 4), wave_instr_per_launch=c["SQ_INSTS_VALU"], source=src)
     clk = c.get("GRBM_GUI_ACTIVE", 0) / 8 / (launch_ms * 1e-3) / 1e9
     # a short launch's GRBM_GUI_ACTIVE also spans its dispatch and drain: a "clock" above
     # the 2.4 GHz maximum is that overhead, not a clock, and is not reported
     if 0 < clk <= 2.4:
         out.update(load_clock_ghz=round(clk, 2), frac_at_load_clock=round(achieved / (VALU_SIMDS * clk / VALU_CYCLES_PER_INSTR), 4))
+    if "SQ_LDS_IDX_ACTIVE" in c:  # LDS-array busy: all LDS cycles / (CUs x launch cycles at the load clock)
+        out["lds_bank_conflict_cycles"] = c.get("SQ_LDS_BANK_CONFLICT")
+        out["lds_array_cycles"] = c["SQ_LDS_IDX_ACTIVE"]
     return out
 
 
-def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms) -> dict:
+def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms, kernels: list) -> dict:
     """C4: the dominant kernel of the iteration (the larger of the fused guide stage and
     the joint bilateral, live event-timed per launch) with its own roof, the other one
     beside it, and the pipeline's HBM rate from the bytes the kernels actually move
@@ -352,8 +366,9 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms)
     nitr, k = cfg["nitr"], cfg["ksize"]
     rj = k - 1                                   # JBF radius: ksize 2k - 1
     taps = circle_taps(rj)
-    guide_k, jbf_k = "void vip::texture_guide_fused_kernel", f"void vip::bilateral_kernel<{rj},"
-    out = {}
+    guide_k = launched(kernels, "void vip::texture_guide_fused_kernel")
+    jbf_k = launched(kernels, f"void vip::bilateral_kernel<{rj},")
+    out = {"kernels": [guide_k, jbf_k]}
     if stage_ms:
         g_ms, j_ms = stage_ms["guide"], stage_ms["jbf"]
         jbf_tf = 8.0 * taps * px / (j_ms * 1e-3) / 1e12
@@ -398,7 +413,7 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms)
     return out
 
 
-def texture_fused_roofline(cfg: dict, px: int, frame_ms: float) -> dict:
+def texture_fused_roofline(cfg: dict, px: int, frame_ms: float, kernels: list) -> dict:
     """C4 in FUSED mode: one launch per iteration (texture_iteration_fused_kernel), so the
     kernel is the whole iteration: FP32 rate of its JBF taps (8 FLOP per in-disc tap, the
     guide stage's work beside it uncounted), VALU issue and HBM traffic from the
@@ -406,10 +421,10 @@ def texture_fused_roofline(cfg: dict, px: int, frame_ms: float) -> dict:
     nitr, k = cfg["nitr"], cfg["ksize"]
     taps = circle_taps(k - 1)
     launch_ms = frame_ms / nitr
-    kern = "void vip::texture_iteration_fused_kernel"
+    kern = launched(kernels, "void vip::texture_iteration_fused_kernel")
     tf = 8.0 * taps * px / (launch_ms * 1e-3) / 1e12
     traffic, tsrc = pmc_traffic("c4fused", [kern])
-    return dict(kernel=f"texture_iteration_fused_kernel (guide + JBF ksize {2 * k - 1} in one launch)",
+    return dict(kernel=f"texture_iteration_fused_kernel (guide + JBF ksize {2 * k - 1} in one launch)", kernel_name=kern,
                 avg_launch_ms=round(launch_ms, 4), bound="valu-fp32", achieved=round(tf, 3), peak=PEAK_FP32_TFLOPS,
                 unit="TFLOP/s", frac=round(tf / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                 traffic_algorithmic=6.0 * px, valu_issue=valu_issue("c4fused", kern, launch_ms),
@@ -526,8 +541,10 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     between barriers + device syncs, max over ranks. Returns the measured quantities."""
     import torch.distributed as dist
 
-    from various_image_processings_amd.filters import _TextureImpl
+    from various_image_processings_amd.filters import _TextureImpl, launched_kernels
     from various_image_processings_amd.sharded import ShardedBilateral, ShardedTexture, exchange_halo
+
+    launched_kernels()  # clear this thread's launch log: the workload below names its kernels
 
     S = len(streams)
     stream = streams[0]
@@ -837,6 +854,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     got = dict(zip(keys, (float(v) for v in t)))
+    res["kernels"] = launched_kernels()  # every kernel instantiation this workload launched
     res.update(elapsed=got["elapsed"], launch_ms=got["launch"], host_s=got["host"], frame_ms=kernel_ms, rows=rows, geo=geo,
                parts={x: got[x] for x in sorted(parts)} if parts else None, native=native, fused=fused)
     return res
@@ -930,21 +948,22 @@ def main():
     value = total_px / (elapsed / args.steps) / 1e6
 
     if m["fused"]:
-        roof = texture_fused_roofline(cfg, px_per_rank, launch_ms)
+        roof = texture_fused_roofline(cfg, px_per_rank, launch_ms, m["kernels"])
     elif cfg["kind"] == "texture":
-        roof = texture_roofline(args.config, cfg, px_per_rank, launch_ms, m["stage_ms"])
+        roof = texture_roofline(args.config, cfg, px_per_rank, launch_ms, m["stage_ms"], m["kernels"])
     else:
         taps = circle_taps(r)
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
         tflops = flops / (launch_ms * 1e-3) / 1e12
         hbm = 6.0 * px_per_rank / (launch_ms * 1e-3) / 1e9
         # the committed PMC summaries are single-GPU whole-frame launches
-        kname = cfg.get("kernel", f"void vip::{cfg['kind']}_kernel<{r},")  # PMC summary lookup
+        # the exact instantiation this run launched (vip_launched_kernels), for the PMC lookup
+        kname = launched(m["kernels"], cfg.get("kernel", f"void vip::{cfg['kind']}_kernel<{r},"))
         traffic, tsrc = (None, None) if sharded else pmc_traffic(args.config, [kname])
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
-                    kernel=cfg.get("kernel_label", f"{cfg['kind']}_kernel<R={r}>"),
+                    kernel=cfg.get("kernel_label", f"{cfg['kind']}_kernel<R={r}>"), kernel_name=kname,
                     avg_launch_ms=round(launch_ms, 4),
                     flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
                     gtaps_per_s=round(taps * px_per_rank / (launch_ms * 1e-3) / 1e9, 1),
@@ -987,6 +1006,7 @@ def main():
                    **({"backend": state.get("backend"), "exchange": m["exchange"]} if state["multi"] else {}),
                    **({"exchange_fallback": m["exchange_fallback"]} if m.get("exchange_fallback") else {})},
         "roofline": roof,
+        "kernels": m["kernels"],
         # per step, max over ranks: one frame on one stream (N>1: with its exchange),
         # event-timed in max(4, K/4) steps after the timed region; the roofline's launch
         # durations come from it

@@ -40,6 +40,12 @@ typedef struct vip_adaptive_s* vip_adaptive_t;
 typedef struct vip_texture_s* vip_texture_t;
 
 int vip_abi_version(void);
+/* The kernels the calling thread launched through this library since its previous call,
+ * as the profiler names them ("void vip::bilateral_kernel<7, 16, ...>", no parameter
+ * list), newline-separated, each once; clears the list. Writes at most len - 1 bytes and a
+ * terminating 0; returns the full length. No reference counterpart: it lets a benchmark
+ * name the exact template instantiation it timed. */
+int vip_launched_kernels(char* buf, size_t len);
 const char* vip_error_string(int code);
 /* Largest filter radius (ksize/2) any filter accepts (32: bilateral ksize 65). */
 int vip_max_radius(void);

@@ -11,8 +11,10 @@ from conftest import ROOT
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-KERNELS = {"c2": "void vip::bilateral_kernel<7,", "c3": "void vip::adaptive_kernel<7,",
-           "c5": "void vip::bilateral_kernel<15,"}
+# exact instantiations (full template signature, as vip_launched_kernels names them) that
+# committed PMC summaries hold
+KERNELS = {"c3": "void vip::adaptive_kernel<7, 16, true, 4, 512, true>",
+           "c5": "void vip::bilateral_kernel<15, 16, false, true, 32, 8, 768, false, 16, false>"}
 
 
 @pytest.mark.parametrize("cfg", sorted(KERNELS))
@@ -35,6 +37,40 @@ def test_valu_issue_roofline_is_consistent(cfg):
     assert v["achieved"] == pytest.approx(v["wave_instr_per_launch"] / (launch_ms * 1e-3) / 1e9, rel=1e-3)
     assert 0.0 < v["frac"] < 1.0
     assert 0.0 < v["frac_at_load_clock"] <= 1.0
+
+
+def test_pmc_lookup_needs_the_exact_signature():
+    """A summary of another instantiation is stale for a bench line: a prefix, a shorter
+    template list (an older build) or another tiling finds nothing."""
+    exact = KERNELS["c5"]
+    assert bench.pmc_traffic("c5", [exact])[0] is not None
+    assert bench.pmc_traffic("c5", ["void vip::bilateral_kernel<15,"]) == (None, None)
+    assert bench.pmc_traffic("c5", [exact[:-1] + ", 7>"]) == (None, None)
+    # round 3's C2 summary was of the 8-argument template; the benched kernel has 10
+    stale = "void vip::bilateral_kernel<7, 16, false, true, 32, 8, 768, false>"
+    e, src = bench.pmc_summary("c2", stale, "traffic_bytes")
+    assert e is not None and src.endswith("r03_c2_pmc.json")
+    assert bench.valu_issue("c2", stale + " ", 0.2) is None
+    assert bench.launched([stale, KERNELS["c5"]], "void vip::bilateral_kernel<15,") == KERNELS["c5"]
+    assert bench.launched([stale], "void vip::adaptive") is None
+
+
+def test_committed_lines_cite_a_summary_of_the_kernel_they_timed():
+    """Every committed bench line that names its kernel (roofline.kernel_name, round 4 on)
+    takes traffic / VALU issue only from a PMC summary holding exactly that kernel."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench.json"))):
+        lines = [ln for ln in open(f).read().splitlines() if ln.startswith("{")]
+        if not lines:
+            continue
+        roof = json.loads(lines[-1]).get("roofline", {})
+        name = roof.get("kernel_name")
+        if not name:
+            continue
+        for src in filter(None, [roof.get("traffic_source"), (roof.get("valu_issue") or {}).get("source")]):
+            for one in src.split(", "):
+                with open(os.path.join(ROOT, one)) as fh:
+                    assert name in json.load(fh)["kernels"], (f, one, name)
 
 
 def test_committed_bench_lines_carry_the_contract_fields():

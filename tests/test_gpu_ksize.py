@@ -230,3 +230,15 @@ def test_texture_handle_allocates_no_f32_scratch(dev):
     # + the embedded JBF handle's LUT and tables (< 1 MiB) and allocator granularity
     assert want <= used <= want + 8 * 2 ** 20, (used, want)
     del t
+
+
+@pytest.mark.parametrize("k", list(range(2, 25, 2)))
+def test_texture_every_even_k_follows_include_cpp(dev, oracle, k):
+    """Even texture ksize: the include/cpp semantics (a (k+1)x(k+1) window, the box sum
+    over k*k, sigma_alpha 1/(5k); include/cpp/bilateral_texture_filter.hpp:41-59), which
+    the oracle restates (tests/test_oracle.py::test_numpy_restatement_blur_rtv_guide); the
+    reference's CUDA stages read one column past their tile there (undefined)."""
+    img = _img(oracle, 41, 67)
+    got = _run_texture(dev, img, k, 2)
+    want = oracle.texture(img, k, 2)
+    assert np.array_equal(got, want), _mismatch(got, want)

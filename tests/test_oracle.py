@@ -131,10 +131,16 @@ def test_numpy_restatement_gradient(oracle):
             assert np.array_equal(np.sqrt(s), oracle.gradient(a, profile=oracle.CPP))
 
 
-def test_numpy_restatement_blur_rtv_guide(oracle):
+@pytest.mark.parametrize("k", [5, 4, 6])
+def test_numpy_restatement_blur_rtv_guide(oracle, k):
+    """Odd and EVEN k. Even k follows include/cpp/bilateral_texture_filter.hpp:41-59 and
+    :98-101: the window is +-(k / 2), i.e. (k + 1) x (k + 1) taps, the box sum is divided
+    by k * k and sigma_alpha is 1 / (5k). (The reference's CUDA stages use the same
+    window but size their tile for k - 1 apron columns,
+    src/bilateral_texture_filter_impl.cu:28,80-85: undefined there.)"""
     img = oracle.random_image(31, 19)
     mag = oracle.random_f32(31 * 19).reshape(19, 31)
-    k, r = 5, 2
+    r = k // 2
     b, rtv = oracle.blur_rtv(img, mag, k, oracle.CUDA)
     h, w = mag.shape
     ys, xs = np.arange(h), np.arange(w)

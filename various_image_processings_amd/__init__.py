@@ -25,6 +25,7 @@ from .filters import (  # noqa: F401
     DeviceImage,
     cuda_gradient,
     device_synchronize,
+    launched_kernels,
     max_ksize,
     set_bilateral_waves,
     set_bilateral_wide,

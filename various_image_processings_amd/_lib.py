@@ -30,6 +30,7 @@ _c_size_t = ctypes.c_size_t
 # name -> (restype, argtypes); every entry point declared in include/vip.h
 SIGNATURES = {
     "vip_abi_version": (_c_int, []),
+    "vip_launched_kernels": (_c_int, [ctypes.c_char_p, _c_size_t]),
     "vip_error_string": (ctypes.c_char_p, [_c_int]),
     "vip_max_radius": (_c_int, []),
     "vip_max_ksize": (_c_int, [_c_int]),

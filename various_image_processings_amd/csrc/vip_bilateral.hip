@@ -359,6 +359,7 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs, SAT)) return rc;
+    note_launch(reinterpret_cast<const void*>(kern));
     StencilArgs args = a;
     args.tiles_x = (a.width + G::TW - 1) / G::TW;
     args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);

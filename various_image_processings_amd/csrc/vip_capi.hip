@@ -10,7 +10,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <cxxabi.h>
 #include <new>
+#include <string>
 
 #include "vip_stencil.hpp"
 
@@ -230,7 +232,42 @@ static RtArgs rt_args(const RtTables& t, int radius, int width, const uint8_t* s
     return a;
 }
 
+namespace {
+thread_local const void* g_launched[16];  // distinct kernels launched since the last query
+thread_local int g_nlaunched = 0;
+}  // namespace
+
+namespace vip {
+void note_launch(const void* kern) {
+    for (int i = 0; i < g_nlaunched; ++i)
+        if (g_launched[i] == kern) return;
+    if (g_nlaunched < 16) g_launched[g_nlaunched++] = kern;
+}
+}  // namespace vip
+
 extern "C" {
+
+int vip_launched_kernels(char* buf, size_t len) {
+    std::string all;
+    for (int i = 0; i < g_nlaunched; ++i) {
+        const char* mangled = hipKernelNameRefByPtr(g_launched[i], nullptr);
+        if (!mangled) continue;
+        int st = 0;
+        char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+        std::string name = st == 0 && dem ? dem : mangled;
+        std::free(dem);
+        const size_t paren = name.find('(');
+        if (paren != std::string::npos) name.resize(paren);  // the profiler summaries' key: no parameter list
+        all += (all.empty() ? "" : "\n") + name;
+    }
+    g_nlaunched = 0;
+    if (buf && len) {
+        const size_t n = all.size() < len - 1 ? all.size() : len - 1;
+        std::memcpy(buf, all.data(), n);
+        buf[n] = 0;
+    }
+    return (int)all.size();
+}
 
 int vip_abi_version(void) { return VIP_ABI_VERSION; }
 int vip_max_radius(void) { return kRtMaxRadius; }

@@ -87,6 +87,11 @@ inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned 
     return 0;
 }
 
+// Launch log of the calling thread (vip_launched_kernels, vip_capi.hip): every stencil and
+// texture-stage kernel notes its host stub before its launch, so a caller can name the
+// exact template instantiation it timed (bench.py matches it against PMC summaries).
+void note_launch(const void* kern);
+
 // vip_bilateral_set_waves (vip_capi.hip): 0 = per-launch choice, else 16 / 8 / 4.
 int bilateral_forced_waves();
 // vip_bilateral_set_wide: 0 = per-launch choice, 1 = 128-pixel tiles (8 outputs per

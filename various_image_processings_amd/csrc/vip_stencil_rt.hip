@@ -271,6 +271,7 @@ static int launch_rt_c(const RtArgs& a, int lds, hipStream_t stream) {
     auto kern = stencil_rt_kernel<COPIES, JOINT, FMA, ADAPTIVE>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), kLdsBudget, attr_devs)) return rc;
+    note_launch(reinterpret_cast<const void*>(kern));
     const int tiles_y = (a.out_rows + kRtWaves * 4 - 1) / (kRtWaves * 4);
     const long long tiles = (long long)a.tiles_x * tiles_y;
     if (tiles == 0) return 0;

@@ -423,7 +423,11 @@ __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restr
                 raw[k][2] = (g ^ 7) * 0x01010101u;
             } else
 #endif
+#ifdef VIP_GF_ISA_HOT  // ISA-count builds only (scripts/isa_classes.py): the interior path alone
+            if (true) {
+#else
             if ((aligned & 1) && x >= 0 && x + 3 <= W1) {
+#endif
                 const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
                 raw[k][0] = w[0];
                 raw[k][1] = w[1];
@@ -538,7 +542,11 @@ VIP_GF_STAMP(8);
         const int ix = x0 - R + c, iy0 = y0 - R + p0;
         uint32_t s0[kGfV2], s1[kGfV2], s2[kGfV2], smx[kGfV2];
         float mmax[kGfV2], msum[kGfV2];
+#ifdef VIP_GF_ISA_HOT
+        if (true) {
+#else
         if (ix >= 0 && ix <= W1 && iy0 >= H0 && iy0 + kGfV2 - 1 <= H1) {
+#endif
             constexpr int NV = kGfV2 + K - 1;
             uint32_t hrb[NV], hg[NV], hmx[NV];
             // magnitudes are finite and >= +0: their bit patterns order like their values, so
@@ -840,6 +848,7 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int 
     auto kern = texture_guide_fused_kernel<R, CPP>;
     static std::atomic<unsigned long long> attr_devs{0};
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs)) return rc;
+    note_launch(reinterpret_cast<const void*>(kern));
     if (gy1 <= gy0) return 0;
     dim3 grid((width + G::TW - 1) / G::TW, (gy1 - gy0 + G::TH - 1) / G::TH);
     hipLaunchKernelGGL(kern, grid, dim3(G::NT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
@@ -1012,6 +1021,7 @@ int launch_texture_iteration_fused(const StencilArgs& a, int ksize, bool cpp, hi
     static std::atomic<unsigned long long> attr_devs[2];
     if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), kFuLds, attr_devs[cpp ? 1 : 0]))
         return rc;
+    note_launch(reinterpret_cast<const void*>(kern));
     StencilArgs args = a;
     args.tiles_x = (a.width + FuJG::TW - 1) / FuJG::TW;
     args.tiles_total = args.tiles_x * ((a.out_rows + kFuTH - 1) / kFuTH);

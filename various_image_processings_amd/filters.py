@@ -29,7 +29,7 @@ from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
 __all__ = [
     "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
     "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
-    "set_bilateral_waves", "set_bilateral_wide", "set_stencil_path", "max_ksize",
+    "set_bilateral_waves", "set_bilateral_wide", "launched_kernels", "set_stencil_path", "max_ksize",
 ]
 
 
@@ -97,6 +97,16 @@ def set_bilateral_wide(mode: int = 0) -> None:
     per launch, 1 = 128-pixel tiles (8 outputs per thread), 2 = 256-pixel tiles (one row
     per wave, 4 outputs per thread). Outputs are identical for every setting."""
     call("vip_bilateral_set_wide", int(mode))
+
+
+def launched_kernels() -> list:
+    """include/vip.h vip_launched_kernels: the kernels this thread launched through the
+    library since the previous call, as the profiler names them (template arguments, no
+    parameter list); clears the list."""
+    n = lib().vip_launched_kernels(None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    lib().vip_launched_kernels(buf, n + 1)
+    return [x for x in buf.value.decode().split("\n") if x]
 
 
 def set_bilateral_waves(waves: int = 0) -> None:
