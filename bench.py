@@ -180,7 +180,7 @@ def parse():
     p.add_argument("--texture-mode", default="two-launch", choices=["two-launch", "fused"])
     # frames in flight: step i runs on HIP stream i % S (one filter handle per stream
     # where the handle owns scratch), so one frame's kernel tails and launch gaps overlap
-    # the next frame's start. Measured (scripts/stream_bench.py, steady clocks): C2
+    # the next frame's start. Measured (scripts/experiments/stream_bench.py, steady clocks): C2
     # 0.178 -> 0.173 ms, C3 0.327 -> 0.323, C4 0.717 -> 0.641 ms per frame with 2; 3 no
     # better. S must divide the 12 rotating buffers (a buffer always meets the same stream)
     p.add_argument("--streams", type=int, default=None, choices=[1, 2, 3, 4, 6],

@@ -1,6 +1,6 @@
 """C4 (texture k=5 nitr=5, 4K) per-frame time with S frames in flight on S streams, for
 alternative library builds (each in its own subprocess).
-usage: python scripts/c4_inflight_bench.py lib1.so [lib2.so ...]"""
+usage: python scripts/experiments/c4_inflight_bench.py lib1.so [lib2.so ...]"""
 import os
 import subprocess
 import sys

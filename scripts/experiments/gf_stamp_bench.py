@@ -3,7 +3,7 @@ Runs one 4K k=5 iteration, reads [workgroup][wave][8] shader-clock stamps (entry
 at each of the 6 phase barriers, exit) and prints, per phase, the mean duration from the
 previous barrier's last arrival to each wave's arrival (work) and to the last wave's
 arrival (phase length, i.e. incl. the wait for the slowest wave).
-usage: python scripts/gf_stamp_bench.py variants/<stamps>.so"""
+usage: python scripts/experiments/gf_stamp_bench.py variants/<stamps>.so"""
 import ctypes
 import json
 import sys

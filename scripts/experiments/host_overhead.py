@@ -1,7 +1,7 @@
 """Host time per launch of the C1 bilateral (512x512, ksize 11) through each Python
 layer, without synchronising inside the loop (the queue absorbs the launches): the
 bench path (ShardedBilateral.filter), the handle's run_rows, and a bare ctypes call
-of vip_bilateral_run_rows with pre-converted arguments. usage: python scripts/host_overhead.py"""
+of vip_bilateral_run_rows with pre-converted arguments. usage: python scripts/experiments/host_overhead.py"""
 import json
 import sys
 import time

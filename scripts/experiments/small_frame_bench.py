@@ -2,7 +2,7 @@
 (VIP_BIL_WAVES=16|8|4 x VIP_BIL_WIDE=1 (128-px tiles) | 2 (256-px tiles), or the
 library's own choice), one subprocess per setting (the knobs are read once per process). Every forced setting's output must equal the
 auto setting's byte for byte (same arithmetic, different tiles).
-usage: python scripts/small_frame_bench.py [out.json]"""
+usage: python scripts/experiments/small_frame_bench.py [out.json]"""
 import json
 import os
 import subprocess

@@ -11,7 +11,7 @@ import time
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from various_image_processings_amd.filters import _AdaptiveImpl, _BilateralImpl, _TextureImpl  # noqa: E402
 
 W, H, NBUF = 3840, 2160, 12

@@ -20,6 +20,9 @@
 #   gloo=CFG,N          python bench.py --gpus N --same-device --backend gloo (N ranks on cuda:0)
 #                                               -> ${TAG}_CFG_gloo{N}.json
 #   py=SCRIPT[,A,..]    python SCRIPT A..       -> ${TAG}_<script name>.txt
+#                       (the one-off measurements behind DESIGN.md's tables: scripts/experiments/)
+#   variants            variant libraries (variants/*.so from build_variant.sh / build_texture_variant.sh):
+#                       parity against the oracle, then timing -> ${TAG}_variants.log
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -85,6 +88,14 @@ for step in "$@"; do
       s=${A[0]}; out=$O/${TAG}_$(basename ${s%.*}).txt
       timeout -k 10 600 python $s "${A[@]:1}" > $out 2>&1
       rc=$?; tail -30 $out; [ $rc -eq 0 ] || fail "$step" $rc ;;
+    variants)
+      log=$O/${TAG}_variants.log; : > $log
+      for so in variants/*.so; do
+        timeout -k 10 300 python scripts/variant_parity.py $so >> $log 2>&1
+        rc=$?; echo "parity $so rc=$rc"; [ $rc -eq 0 ] || fail "$step parity $so" $rc $log
+      done
+      timeout -k 10 600 python scripts/variant_bench.py variants/*.so >> $log 2>&1
+      rc=$?; tail -30 $log; [ $rc -eq 0 ] || fail "$step" $rc ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
