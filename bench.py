@@ -203,6 +203,9 @@ def parse():
     # the real exchange, its trial forms and graph replay run on one GPU. One rank's slab:
     # not a scaling number.
     p.add_argument("--loopback", type=int, default=0, metavar="N")
+    # N > 1 native: also time each frame replayed from a captured hipGraph (vip_shard_set_graph)
+    # in the split / batch trial
+    p.add_argument("--graph", action=argparse.BooleanOptionalAction, default=False)
     # --gpus N > 1 without WORLD_SIZE in the environment: this process starts the N ranks
     # itself (a child torchrun) and ends them after this many seconds
     p.add_argument("--launch-timeout", type=float, default=LAUNCH_TIMEOUT_S)
@@ -729,7 +732,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         batches = halo_batches(S)
         forms = []
         for split in ((False,) if cfg["kind"] == "texture" else (True, False)):
-            forms += [(split, b, False) for b in batches] + [(split, 1, True)]
+            forms += [(split, b, False) for b in batches] + ([(split, 1, True)] if args.graph else [])
         for split, b, graph in forms:
             for x in shards:
                 x.set_split(split)

@@ -15,7 +15,7 @@
 #   stats=CFG[,A,..]    rocprofv3 --kernel-trace --stats of a short bench run
 #                                               -> ${TAG}_CFG_kernel_stats.csv, ${TAG}_CFG_busy.json
 #   pmc=CFG[,A,..]      one rocprofv3 --pmc pass per counter set -> ${TAG}_CFG_pmc.json
-#   rehearse=CFG,N      the N > 1 native path on one GPU: bench.py --rehearse-native --loopback N
+#   rehearse=CFG,N[,A]  the N > 1 native path on one GPU: bench.py --rehearse-native --loopback N A..
 #                                               -> ${TAG}_CFG_loopbackN.json
 #   gloo=CFG,N          python bench.py --gpus N --same-device --backend gloo (N ranks on cuda:0)
 #                                               -> ${TAG}_CFG_gloo{N}.json
@@ -76,13 +76,13 @@ for step in "$@"; do
       python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json | cut -c1-400 || fail "$step" $? ;;
     rehearse)
       cfg=${A[0]}; n=${A[1]}; out=$O/${TAG}_${cfg}_loopback$n.json
-      timeout -k 10 400 python bench.py --config $cfg --rehearse-native --loopback $n --steps ${A[2]:-400} \
+      timeout -k 10 400 python bench.py --config $cfg --rehearse-native --loopback $n --steps 400 "${A[@]:2}" \
         > $out 2> $O/${TAG}_${cfg}_loopback$n.err
       rc=$?; cut -c1-1500 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_loopback$n.err ;;
     gloo)
       cfg=${A[0]}; n=${A[1]}; out=$O/${TAG}_${cfg}_gloo$n.json
-      timeout -k 10 500 python bench.py --gpus $n --same-device --backend gloo --config $cfg --steps ${A[2]:-8} \
-        --warmup 1 > $out 2> $O/${TAG}_${cfg}_gloo$n.err
+      timeout -k 10 500 python bench.py --gpus $n --same-device --backend gloo --config $cfg --steps 8 \
+        --warmup 1 "${A[@]:2}" > $out 2> $O/${TAG}_${cfg}_gloo$n.err
       rc=$?; cut -c1-800 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_gloo$n.err ;;
     py)
       s=${A[0]}; out=$O/${TAG}_$(basename ${s%.*}).txt

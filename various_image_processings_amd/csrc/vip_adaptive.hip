@@ -76,7 +76,11 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     const int tx = lane & 15;
     const int ty = wave * 4 + (lane >> 4);
     const uint32_t lane16 = (uint32_t)(lane & (COPIES - 1)) << 2;
+#if VIP_SAT_SHARE31  // measurement knob: lanes 30/31 share copy 30, copy 31's bank holds only the saturation target
+    const uint32_t sbias = (uint32_t)kAdaSatB0 + (COPIES == 32 && lane16 == 124u ? 120u : lane16);
+#else
     const uint32_t sbias = (uint32_t)kAdaSatB0 + lane16;  // SAT: register bias of the address
+#endif
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x

@@ -99,7 +99,11 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     const int tx = lane % TPR;
     const int ty = wave * G::RPW + lane / TPR;
     const uint32_t lane4 = (uint32_t)(lane & (COPIES - 1)) << 2;  // this lane's LUT copy
+#if VIP_SAT_SHARE31  // measurement knob: lanes 30/31 share copy 30, copy 31's bank holds only the saturation target
+    const uint32_t sbias = (uint32_t)SL::B0 + (SAT && COPIES == 32 && lane4 == 124u ? 120u : lane4);
+#else
     const uint32_t sbias = (uint32_t)SL::B0 + lane4;                // SAT: register bias of the address
+#endif
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     VIP_RT_STAMP(0);
