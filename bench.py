@@ -858,6 +858,11 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     got = dict(zip(keys, (float(v) for v in t)))
     res["kernels"] = launched_kernels()  # every kernel instantiation this workload launched
+    if native:  # release the communicators on every rank at the same point (not at GC time)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        for x in shards:
+            x.close()
     res.update(elapsed=got["elapsed"], launch_ms=got["launch"], host_s=got["host"], frame_ms=kernel_ms, rows=rows, geo=geo,
                parts={x: got[x] for x in sorted(parts)} if parts else None, native=native, fused=fused)
     return res

@@ -409,12 +409,17 @@ class NativeShard:
         S.call("vip_shard_run_timed", self._h, _ptr(slab, p * self.geo.slab_rows), _ptr(out, p * self.geo.own), p,
                _stream(stream), arr)
 
+    def close(self) -> None:
+        """vip_shard_destroy now (releases the communicator: call it at the same point on
+        every rank rather than leaving it to the garbage collector)."""
+        if self._h and self._h.value:
+            from . import _shard_lib as S
+            S.lib().vip_shard_destroy(self._h)
+        self._h = None
+
     def __del__(self):
         try:
-            if self._h and self._h.value:
-                from . import _shard_lib as S
-                S.lib().vip_shard_destroy(self._h)
-                self._h = None
+            self.close()
         except Exception:
             pass
 
