@@ -581,3 +581,20 @@ def test_frames_in_flight_on_two_streams(dev, oracle, kind):
     for i in range(6):
         got = dev.get(dsts[i])
         assert np.array_equal(got, want[i]), f"frame {i}: " + _mismatch(got, want[i])
+
+
+def test_launched_kernels_names_the_instantiation(dev, oracle):
+    """vip_launched_kernels: the exact template instantiation of each launch, as rocprofv3
+    names it (profiles/r03_c2_busy.json holds the C2 one), each once, cleared per call."""
+    vip.launched_kernels()
+    img = oracle.random_image(3840, 2160)
+    d = dev.empty((2160, 3840, 3))
+    f = vip.CudaBilateralFilter(3840, 2160, 15)
+    f.bilateral_filter(dev.put(img), d)
+    f.bilateral_filter(dev.put(img), d)
+    assert vip.launched_kernels() == ["void vip::bilateral_kernel<7, 16, false, true, 32, 8, 768, false, 16, false>"]
+    assert vip.launched_kernels() == []
+    vip.CudaBilateralTextureFilter(300, 200, 5, 2).execute(dev.put(img[:200, :300].copy()), dev.empty((200, 300, 3)))
+    names = vip.launched_kernels()
+    assert len(names) == 2 and any(n.startswith("void vip::texture_guide_fused_kernel<2, false>") for n in names)
+    assert all("(" not in n for n in names)
