@@ -42,8 +42,9 @@ typedef struct vip_texture_s* vip_texture_t;
 int vip_abi_version(void);
 /* The kernels the calling thread launched through this library since its previous call,
  * as the profiler names them ("void vip::bilateral_kernel<7, 16, ...>", no parameter
- * list), newline-separated, each once; clears the list. Writes at most len - 1 bytes and a
- * terminating 0; returns the full length. No reference counterpart: it lets a benchmark
+ * list), newline-separated, each once. With a buffer (len > 0) it writes at most len - 1
+ * bytes and a terminating 0 and clears the list; buf = NULL, len = 0 only returns the
+ * length. Returns the full length. No reference counterpart: it lets a benchmark
  * name the exact template instantiation it timed. */
 int vip_launched_kernels(char* buf, size_t len);
 const char* vip_error_string(int code);

@@ -2,17 +2,24 @@
 torch's own copies, which libvip_shard.so's symbols bind to): loopback shards, one per
 stream, frames replayed from captured graphs against their direct runs. Run in a child
 process of its own (a crash here ends only this probe).
-usage: python scripts/experiments/graph_probe.py [split]"""
+usage: python scripts/experiments/graph_probe.py [split] [trace] [sysrccl]"""
 import faulthandler
 import sys
 
 sys.path.insert(0, ".")
 faulthandler.enable()
+if "trace" in sys.argv:  # native backtrace of a crash (microbench/segv_trace.c)
+    import ctypes
+    ctypes.CDLL("microbench/libsegv_trace.so").segv_trace_install()
+if "sysrccl" in sys.argv:  # the system HIP 7.2 + RCCL 2.27.7 loaded before torch's own copies
+    import ctypes
+    for lib in ("/opt/rocm/lib/libamdhip64.so.7", "/opt/rocm/lib/librccl.so.1"):
+        ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
 import torch  # noqa: E402
 
 from various_image_processings_amd.sharded import NativeShard  # noqa: E402
 
-split = len(sys.argv) > 1 and sys.argv[1] == "split"
+split = "split" in sys.argv[1:]
 torch.cuda.set_device(0)
 w, own, n = 3840, 270, 8
 streams = [torch.cuda.Stream(), torch.cuda.Stream()]

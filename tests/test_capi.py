@@ -192,3 +192,26 @@ def test_shard_create_validates_before_device_work():
     assert L.vip_shard_create(*args(0, 100, 15, 2, 2)) == 10001      # rank outside the world
     assert L.vip_shard_create(*args(0, 100, 8, 2, 0)) == 10002       # even ksize
     assert L.vip_shard_create(ctypes.byref(h), 0, 64, 100, 15, 10.0, 30.0, 0, 2, 0, None, 1000) == 10001
+
+
+def test_launch_log_names_kernels_like_the_profiler():
+    """vip_launched_kernels (no GPU needed): a kernel handle noted by the launch path comes
+    back as the profiler names it (demangled, template arguments, no parameter list), each
+    once; a size query keeps the list, a read clears it."""
+    import ctypes
+    from various_image_processings_amd import _lib
+    from various_image_processings_amd.filters import launched_kernels
+    lib = _lib.lib()
+    libdl = ctypes.CDLL(None)
+    libdl.dlsym.restype = ctypes.c_void_p
+    libdl.dlsym.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+    handle = libdl.dlsym(lib._handle, b"_ZN3vip16bilateral_kernelILi7ELi16ELb0ELb1ELi32ELi8ELi768ELb0ELi16ELb0EEEvNS_11StencilArgsE")
+    assert handle
+    note = lib._ZN3vip11note_launchEPKv
+    note.argtypes = [ctypes.c_void_p]
+    launched_kernels()
+    note(handle)
+    note(handle)
+    assert lib.vip_launched_kernels(None, 0) > 0
+    assert launched_kernels() == ["void vip::bilateral_kernel<7, 16, false, true, 32, 8, 768, false, 16, false>"]
+    assert launched_kernels() == []

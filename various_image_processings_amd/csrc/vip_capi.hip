@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cxxabi.h>
+#include <dlfcn.h>
 #include <new>
 #include <string>
 
@@ -250,7 +251,12 @@ extern "C" {
 int vip_launched_kernels(char* buf, size_t len) {
     std::string all;
     for (int i = 0; i < g_nlaunched; ++i) {
-        const char* mangled = hipKernelNameRefByPtr(g_launched[i], nullptr);
+        // the kernel handle is an exported symbol of this library: its name is the kernel's
+        // mangled name (dladdr); the runtime's lookup is the fallback (some runtimes return null)
+        Dl_info info{};
+        const char* mangled = dladdr(g_launched[i], &info) && info.dli_sname && info.dli_saddr == g_launched[i]
+                                  ? info.dli_sname
+                                  : hipKernelNameRefByPtr(g_launched[i], nullptr);
         if (!mangled) continue;
         int st = 0;
         char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
@@ -260,8 +266,8 @@ int vip_launched_kernels(char* buf, size_t len) {
         if (paren != std::string::npos) name.resize(paren);  // the profiler summaries' key: no parameter list
         all += (all.empty() ? "" : "\n") + name;
     }
-    g_nlaunched = 0;
     if (buf && len) {
+        g_nlaunched = 0;  // a size query (no buffer) keeps the list
         const size_t n = all.size() < len - 1 ? all.size() : len - 1;
         std::memcpy(buf, all.data(), n);
         buf[n] = 0;
