@@ -105,6 +105,21 @@ def launch_ranks(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script
         return 124
 
 
+SYSTEM_ROCM = ("/opt/rocm/lib/libamdhip64.so.7", "/opt/rocm/lib/librccl.so.1")
+
+
+def preload_system_rocm() -> None:
+    """--graph: load the image's ROCm HIP runtime and RCCL (7.2 / 2.27.7) into the global
+    symbol scope BEFORE torch, so torch and the library share them. torch's bundled RCCL
+    2.26.6 crashes when an RCCL group is captured into a hipGraph (measured in every capture
+    mode, profiles/r04_graph_capture.txt); the image's RCCL captures and replays correctly
+    (tests/cpp/shard_graph_test). torch's own copies still load beside them (their file
+    names differ), so the process ends with os._exit once its line is printed."""
+    import ctypes
+    for lib in SYSTEM_ROCM:
+        ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
+
+
 def halo_batches(streams: int) -> list:
     """Frames per RCCL group the N > 1 native path may use with this many streams: frame i
     runs in batch i // B on stream (i // B) % S, so B * S must divide NBUF for buffer
@@ -204,7 +219,8 @@ def parse():
     # not a scaling number.
     p.add_argument("--loopback", type=int, default=0, metavar="N")
     # N > 1 native: also time each frame replayed from a captured hipGraph (vip_shard_set_graph)
-    # in the split / batch trial
+    # in the split / batch trial; loads the image's HIP runtime and RCCL before torch
+    # (preload_system_rocm)
     p.add_argument("--graph", action=argparse.BooleanOptionalAction, default=False)
     # --gpus N > 1 without WORLD_SIZE in the environment: this process starts the N ranks
     # itself (a child torchrun) and ends them after this many seconds
@@ -876,6 +892,8 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.rehearse_native:
         # plain `python bench.py --gpus N`: start the N ranks (nothing has touched the GPU)
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
+    if args.graph:
+        preload_system_rocm()
     import torch
     import torch.distributed as dist
 
@@ -1042,6 +1060,10 @@ def main():
         print(json.dumps(out), flush=True)
     if state["multi"]:
         dist.destroy_process_group()
+    if args.graph:  # two HIP runtimes are loaded (preload_system_rocm): skip their destructors
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
 
 
 if __name__ == "__main__":

@@ -9,7 +9,8 @@
 # be judged into profiles/).
 #
 # STEP
-#   tests[=ARGS]        python -m pytest -m gpu ARGS (default: tests, the whole GPU suite)
+#   tests[=ARGS]        python -m pytest -m gpu ARGS (default: tests, the whole GPU suite; ARGS is
+#                       shell-quoted, e.g. tests="tests/test_gpu_parity.py -k 'texture or gradient'")
 #   smoke               __graft_entry__.smoke()
 #   bench=CFG[,A,..]    bench line              -> ${TAG}_CFG_bench.json (A: extra bench.py args)
 #   stats=CFG[,A,..]    rocprofv3 --kernel-trace --stats of a short bench run
@@ -46,8 +47,8 @@ for step in "$@"; do
   case $name in
     tests)
       log=$O/${TAG}_pytest_gpu.log
-      timeout -k 10 1100 python -u -m pytest ${arg:-tests} -m gpu -v -x -rf --durations=15 --timeout 300 \
-        --timeout-method thread > $log 2>&1
+      eval "timeout -k 10 1100 python -u -m pytest ${arg:-tests} -m gpu -v -x -rf --durations=15 --timeout 300 \
+        --timeout-method thread" > $log 2>&1
       rc=$?; tail -8 $log; [ $rc -eq 0 ] || fail "$step" $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/${TAG}_smoke.log 2>&1

@@ -314,6 +314,17 @@ void free_graphs(vip_shard_s* h) {
 
 constexpr size_t kMaxGraphs = 64;  // captured (slab, out, stream) combinations kept per shard
 
+// Capture mode of graph mode: thread-local by default; VIP_SHARD_CAPTURE_MODE=1 global,
+// 2 relaxed (a measurement knob for RCCL builds that treat the modes differently).
+hipStreamCaptureMode capture_mode() {
+    static const hipStreamCaptureMode m = [] {
+        const char* e = std::getenv("VIP_SHARD_CAPTURE_MODE");
+        const int v = e ? std::atoi(e) : 0;
+        return v == 1 ? hipStreamCaptureModeGlobal : v == 2 ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal;
+    }();
+    return m;
+}
+
 }  // namespace
 
 extern "C" {
@@ -617,7 +628,7 @@ static int run_graph(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
         h->graphs.erase(h->graphs.begin());
     }
     // nothing is enqueued yet: if the stream cannot capture, run this frame directly
-    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    if (hipStreamBeginCapture(s, capture_mode()) != hipSuccess) {
         (void)hipGetLastError();
         return enqueue_run(h, slab, out, out_pitch, s, nullptr);
     }
