@@ -76,10 +76,10 @@ for step in "$@"; do
       done
       python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json | cut -c1-400 || fail "$step" $? ;;
     rehearse)
-      cfg=${A[0]}; n=${A[1]}; out=$O/${TAG}_${cfg}_loopback$n.json
+      cfg=${A[0]}; n=${A[1]}; sfx=$(printf '%s' "${A[*]:2}" | tr -c 'a-zA-Z0-9' '_'); out=$O/${TAG}_${cfg}_loopback$n$sfx.json
       timeout -k 10 400 python bench.py --config $cfg --rehearse-native --loopback $n --steps 400 "${A[@]:2}" \
-        > $out 2> $O/${TAG}_${cfg}_loopback$n.err
-      rc=$?; cut -c1-1500 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_loopback$n.err ;;
+        > $out 2> ${out%.json}.err
+      rc=$?; cut -c1-1500 $out; [ $rc -eq 0 ] || fail "$step" $rc ${out%.json}.err ;;
     gloo)
       cfg=${A[0]}; n=${A[1]}; out=$O/${TAG}_${cfg}_gloo$n.json
       timeout -k 10 500 python bench.py --gpus $n --same-device --backend gloo --config $cfg --steps 8 \
