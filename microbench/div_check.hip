@@ -14,6 +14,10 @@
 //     texture guide's blend: v in [-255, 511]).
 // (e) vip::exp_tab_f32 against (float)exp((double)x) (ocml's double exp) for every float x
 //     in [0, 32) (the texture guide's alpha argument lies in [0, 25.5]).
+// (f) vip::rtv_quotient(n, d) against (float)(n / d) for 2^30 pseudo-random inputs: half
+//     the guide stage's own (n a float in [0, 2^18), d = (double)msum + 1e-9 with msum a
+//     float in [0, 2^19)), half with n / d placed within +-80 double ulps of a float
+//     rounding midpoint (the fallback's territory).
 // Exit status 0 iff no mismatch against the IEEE divide / sqrt (hipcc default, correctly
 // rounded). Run on the GPU: tests/test_gpu_parity.py::test_epilogue_division_exact.
 #include <hip/hip_runtime.h>
@@ -23,7 +27,7 @@
 
 #include "vip_stencil.hpp"
 
-__device__ unsigned long long g_bad[5];
+__device__ unsigned long long g_bad[6];
 __device__ unsigned int g_exp_bad_x[16];
 
 __global__ void exp_all(uint32_t n) {
@@ -94,8 +98,27 @@ __global__ void quot_random(uint64_t base) {
     if (__float_as_uint(q) != __float_as_uint(want)) atomicAdd(&g_bad[1], 1ull);
 }
 
+__global__ void rtv_random(uint64_t base) {
+    const uint64_t i = base + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const uint32_t a = mix(3 * i), b = mix(3 * i + 1), c = mix(3 * i + 2);
+    const float msum = __uint_as_float(a & 0x7fffffffu) < 524288.0f ? __uint_as_float(a & 0x7fffffffu)
+                                                                      : (float)(a >> 13);  // [0, 2^19)
+    const double d = (double)msum + 1e-9;
+    double n;
+    if (c & 1) {
+        n = (double)((float)(b >> 14) + (float)(b & 0x3fff) * (1.0f / 16384.0f));  // a float in [0, 2^18)
+    } else {
+        // n / d within +-80 double ulps of the midpoint between float m and its successor
+        const float m = (float)(b >> 9) * (1.0f / 64.0f) + __uint_as_float(0x38000000u);
+        const double mid = 0.5 * ((double)m + (double)__uint_as_float(__float_as_uint(m) + 1));
+        const double t = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, mid) + (long long)(c >> 24) - 80);
+        n = t * d;
+    }
+    if (__float_as_uint(vip::rtv_quotient(n, d)) != __float_as_uint((float)(n / d))) atomicAdd(&g_bad[5], 1ull);
+}
+
 int main() {
-    unsigned long long zero[5] = {0, 0, 0, 0, 0};
+    unsigned long long zero[6] = {0, 0, 0, 0, 0, 0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_bad), zero, sizeof(zero)) != hipSuccess) return 2;
     // bit patterns of 1.0f and 2^38: the epilogue's sums of weights lie in [1, 1024), the
     // texture guide's 1 + exp(x) in [2, 2^37) (x <= 25.5 at ksize 2)
@@ -111,17 +134,21 @@ int main() {
     hipLaunchKernelGGL(pack_u8_all, dim3((npk + 255) / 256), dim3(256), 0, 0, npk);
     const uint32_t nexp = 0x42000000u;  // bit patterns of [0, 32)
     hipLaunchKernelGGL(exp_all, dim3((nexp + 255) / 256), dim3(256), 0, 0, nexp);
-    unsigned long long bad[5];
+    for (int rep = 0; rep < 16; ++rep)
+        hipLaunchKernelGGL(rtv_random, dim3((unsigned)(per / 256)), dim3(256), 0, 0, rep * per);
+    unsigned long long bad[6];
     if (hipMemcpyFromSymbol(bad, HIP_SYMBOL(g_bad), sizeof(bad)) != hipSuccess) return 2;
     std::printf("reciprocal: %u floats k in [1, 2^38), %llu mismatches\n", n, bad[0]);
     std::printf("quotient: %llu random (s, k), %llu mismatches\n", (unsigned long long)(16 * per), bad[1]);
     std::printf("integer sqrt: %u integers in [0, 2^20), %llu mismatches\n", nsq, bad[2]);
     std::printf("u8 clamp pack: %u floats |v| < 2048 of each sign, %llu mismatches\n", npk, bad[3]);
     std::printf("exp: %u floats x in [0, 32), %llu mismatches\n", nexp, bad[4]);
+    std::printf("rtv quotient: %llu random (n, d), half at float midpoints, %llu mismatches\n",
+                (unsigned long long)(16 * per), bad[5]);
     if (bad[4]) {
         unsigned int xs[16];
         if (hipMemcpyFromSymbol(xs, HIP_SYMBOL(g_exp_bad_x), sizeof(xs)) == hipSuccess)
             for (unsigned long long j = 0; j < bad[4] && j < 16; ++j) std::printf("  exp mismatch at x = %a\n", (double)__builtin_bit_cast(float, xs[j]));
     }
-    return (bad[0] || bad[1] || bad[2] || bad[3] || bad[4]) ? 1 : 0;
+    return (bad[0] || bad[1] || bad[2] || bad[3] || bad[4] || bad[5]) ? 1 : 0;
 }

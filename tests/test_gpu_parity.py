@@ -477,15 +477,17 @@ def test_epilogue_division_exact():
     recip_exact/div_by_sumk). microbench/div_check checks RN(1/k) for EVERY float k in
     [1, 2^38) (the epilogue's sums of weights and the texture guide's 1 + exp(x) at every
     ksize) and 2^30 quotients against the IEEE divide on the GPU, the texture
-    gradient's sqrt_int_exact against sqrtf for every integer in [0, 2^20), and the guide
-    blend's pack_u8_clamped against the clamp for every float |v| < 2048."""
+    gradient's sqrt_int_exact against sqrtf for every integer in [0, 2^20), the guide
+    blend's pack_u8_clamped against the clamp for every float |v| < 2048, and the rtv
+    quotient (rtv_quotient) against the IEEE double divide on 2^30 inputs, half of them at
+    float rounding midpoints."""
     import os
     import subprocess
     exe = os.path.join(os.path.dirname(__file__), "..", "microbench", "div_check")
     assert os.path.exists(exe), "build first: make -C various_image_processings_amd/csrc"
     r = subprocess.run([exe], capture_output=True, text=True, timeout=100)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(" 0 mismatches") == 5, r.stdout
+    assert r.stdout.count(" 0 mismatches") == 6, r.stdout
 
 
 @pytest.mark.parametrize("k,ss,sc", [(31, 1000.0, 1000.0), (5, 0.1, 0.1), (15, 3.0, 1e4), (7, 1e4, 0.5)])

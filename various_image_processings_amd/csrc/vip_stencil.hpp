@@ -622,6 +622,28 @@ __device__ __forceinline__ float recip_exact(float k) {
     return __builtin_fmaf(__builtin_fmaf(-k, y0, 1.0f), y0, y0);
 }
 
+// (float)(n / d) with the IEEE double quotient: the texture guide stage's rtv (CUDA profile,
+// src/bilateral_texture_filter_impl.cu:99-101), n = (double)num in [0, 2^18), d =
+// (double)msum + 1e-9 in [1e-9, 2^20): no scaling is ever needed. Two Newton steps from
+// v_rcp_f64 give r = 1/d to within a few 2^-53 (the first two steps of the compiler's own
+// f64 division), so q = RN(n r) is within 4 double ulps of n/d, and RN_f(q) equals
+// RN_f(RN_d(n/d)) unless n/d lies within that distance of a float rounding midpoint --
+// which q's 29 low mantissa bits show (midpoint: 2^28). Those lanes (about 2^-23 of them)
+// take the IEEE division. 7 f64 ops + 3 integer ops against the division's 11 f64 ops.
+// microbench/div_check compares it with (float)(n / d) on 2^30 inputs, half of them at
+// midpoints.
+__device__ __forceinline__ float rtv_quotient(double n, double d) {
+    const double r0 = __builtin_amdgcn_rcp(d);
+    double e = __builtin_fma(-d, r0, 1.0);
+    double r = __builtin_fma(r0, e, r0);
+    e = __builtin_fma(-d, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = n * r;
+    const uint32_t lo = (uint32_t)__builtin_bit_cast(unsigned long long, q);
+    if (__builtin_expect(((lo & 0x1fffffffu) - (0x10000000u - 64u)) < 128u, 0)) return (float)(n / d);
+    return (float)q;
+}
+
 // RN(s / k) given y = RN(1/k) (Markstein): q0 = RN(s y) is within 1 ulp of s/k, the
 // residual s - k q0 is exact under fma, and one correction rounds correctly. Needs
 // no over/underflow: s in [0, 255 k], k in [1, 1024). Cross-checked on 2^30 random

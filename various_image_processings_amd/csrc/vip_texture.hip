@@ -531,7 +531,9 @@ VIP_GF_STAMP(8);
     //    MR rows p .. p + 2R, columns c .. c + 2R. Results stay in registers until every
     //    thread is done with H (BR/RR alias it).
     const float kk = (float)(ksize * ksize);
-    const float rkk = 1.f / kk;
+    // == 1.f / kk (RN(1/k) for every float k in [1, 2^38), microbench/div_check), 3 VALU
+    // instead of the IEEE division's ~10
+    const float rkk = recip_exact(kk);
     constexpr float kThird = 0x1.555556p-2f;  // RN(1/3)
     float res[G::IT2][kGfV2][4];
 #pragma unroll
@@ -647,7 +649,7 @@ VIP_GF_STAMP(8);
 #ifdef VIP_GF_ABL_DIV  // timing ablation only (inexact): f32 divide instead of the double one
             res[it][j][3] = num / (msum[j] + 1e-9f);
 #else
-            res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+            res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : rtv_quotient((double)num, (double)msum[j] + 1e-9);
 #endif
         }
     }
@@ -675,7 +677,7 @@ VIP_GF_STAMP(8);
     //    takes kGfRun vertically adjacent outputs: each window row's first argmin is
     //    found once and shared; scanning those rows in order with strict > then
     //    gives the row-major first argmin. Alpha blend per output.
-    const float sigma_alpha = 1.f / (float)(5 * ksize);
+    const float sigma_alpha = recip_exact((float)(5 * ksize));  // == 1.f / (5 ksize), as rkk
     for (int run = tid; run < (G::TH / kGfRun) * G::TW; run += G::NT) {
         const int tx = run % G::TW, ty0 = (run / G::TW) * kGfRun;
         const int x = x0 + tx;
