@@ -533,7 +533,11 @@ VIP_GF_STAMP(8);
     const float kk = (float)(ksize * ksize);
     // == 1.f / kk (RN(1/k) for every float k in [1, 2^38), microbench/div_check), 3 VALU
     // instead of the IEEE division's ~10
+#ifdef VIP_GF_IEEE_DIV  // measurement knob: the round-3 IEEE divisions (same values)
+    const float rkk = 1.f / kk;
+#else
     const float rkk = recip_exact(kk);
+#endif
     constexpr float kThird = 0x1.555556p-2f;  // RN(1/3)
     float res[G::IT2][kGfV2][4];
 #pragma unroll
@@ -649,7 +653,11 @@ VIP_GF_STAMP(8);
 #ifdef VIP_GF_ABL_DIV  // timing ablation only (inexact): f32 divide instead of the double one
             res[it][j][3] = num / (msum[j] + 1e-9f);
 #else
+#ifdef VIP_GF_IEEE_DIV
+            res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+#else
             res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : rtv_quotient((double)num, (double)msum[j] + 1e-9);
+#endif
 #endif
         }
     }
@@ -677,7 +685,11 @@ VIP_GF_STAMP(8);
     //    takes kGfRun vertically adjacent outputs: each window row's first argmin is
     //    found once and shared; scanning those rows in order with strict > then
     //    gives the row-major first argmin. Alpha blend per output.
+#ifdef VIP_GF_IEEE_DIV
+    const float sigma_alpha = 1.f / (float)(5 * ksize);
+#else
     const float sigma_alpha = recip_exact((float)(5 * ksize));  // == 1.f / (5 ksize), as rkk
+#endif
     for (int run = tid; run < (G::TH / kGfRun) * G::TW; run += G::NT) {
         const int tx = run % G::TW, ty0 = (run / G::TW) * kGfRun;
         const int x = x0 + tx;
