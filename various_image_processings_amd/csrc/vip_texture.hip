@@ -533,9 +533,10 @@ VIP_GF_STAMP(8);
     const float kk = (float)(ksize * ksize);
     // == 1.f / kk (RN(1/k) for every float k in [1, 2^38), microbench/div_check), 3 VALU
     // instead of the IEEE division's ~10
-#ifdef VIP_GF_IEEE_DIV  // measurement knob: the round-3 IEEE divisions (same values)
+#ifndef VIP_GF_FAST_DIV
     const float rkk = 1.f / kk;
-#else
+#else  // measurement knob, same values: 3 VALU instead of the IEEE division's ~10, but the
+       // C4 frame measured 0.4 % slower with it and rtv_quotient (profiles/r04_gf_fast_div.txt)
     const float rkk = recip_exact(kk);
 #endif
     constexpr float kThird = 0x1.555556p-2f;  // RN(1/3)
@@ -653,7 +654,7 @@ VIP_GF_STAMP(8);
 #ifdef VIP_GF_ABL_DIV  // timing ablation only (inexact): f32 divide instead of the double one
             res[it][j][3] = num / (msum[j] + 1e-9f);
 #else
-#ifdef VIP_GF_IEEE_DIV
+#ifndef VIP_GF_FAST_DIV
             res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
 #else
             res[it][j][3] = CPP ? num / (msum[j] + 1e-9f) : rtv_quotient((double)num, (double)msum[j] + 1e-9);
@@ -685,7 +686,7 @@ VIP_GF_STAMP(8);
     //    takes kGfRun vertically adjacent outputs: each window row's first argmin is
     //    found once and shared; scanning those rows in order with strict > then
     //    gives the row-major first argmin. Alpha blend per output.
-#ifdef VIP_GF_IEEE_DIV
+#ifndef VIP_GF_FAST_DIV
     const float sigma_alpha = 1.f / (float)(5 * ksize);
 #else
     const float sigma_alpha = recip_exact((float)(5 * ksize));  // == 1.f / (5 ksize), as rkk
