@@ -136,13 +136,13 @@ def circle_taps(r: int) -> int:
 CONFIGS = {
     # C1 is the include/cpp (CPU) plumbing case: cpu_baseline times it; the GPU line is
     # the same filter on the same image through the HIP path
-    # c1: a 512x512 frame fills a quarter of the chip with 16-wave 256-pixel tiles (64
-    # workgroups), so 4 frames in flight on 4 streams run side by side (throughput tiling,
-    # set through vip_bilateral_set_waves/_wide; the library's default tiling minimises the
-    # latency of one frame instead: 256 4-wave tiles, 10.7 against 14.5 us per launch)
+    # c1: 4 frames in flight on 4 streams. The library counts the frames in flight (distinct
+    # streams among its recent launches) and picks the throughput tiling by itself: 16-wave
+    # 256-pixel tiles, 64 workgroups per 512x512 frame, so four frames run side by side (one
+    # frame alone takes 256 4-wave tiles, 10.7 against 14.5 us per launch)
     "c1": dict(kind="bilateral", width=512, frame_height=512, ksize=11, data="lenna", cpu_input="lenna",
-               streams=4, tiling=(16, 2), kernel="void vip::bilateral_kernel<5, 16,",
-               kernel_label="bilateral_kernel<R=5> (16 waves x 256-px tiles, 64 per frame)",
+               streams=4, kernel="void vip::bilateral_kernel<5, 16,",
+               kernel_label="bilateral_kernel<R=5> (16 waves x 256-px tiles, 64 per frame, chosen for 4 frames in flight)",
                workload="bilateral r=5 sigma_s=10 sigma_r=30 lenna 512x512"),
     "c2": dict(kind="bilateral", width=3840, rows_per_rank=2160, ksize=15, workload="bilateral r=7 3840x2160 RGB8"),
     "c3": dict(kind="adaptive", width=3840, rows_per_rank=2160, ksize=15,
@@ -843,6 +843,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             # frames on ONE stream, back to back, after the timed region (the S-stream
             # launches overlap, so their event spans are not launch durations)
             n1 = max(4, args.steps // 4)
+            timed_kernels = set(launched_kernels())
+            res["kernels_timed"] = sorted(timed_kernels)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for i in range(n1):
@@ -850,6 +852,24 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             e1.record(stream)
             torch.cuda.synchronize(dev)
             single_ms = e0.elapsed_time(e1) / n1
+            if not set(launched_kernels()) <= timed_kernels:
+                # one stream made the library pick another tiling than the frames in flight
+                # did (its small-frame tiling counts the streams in use): time the timed
+                # region's kernel instead, one launch at a time but rotating over the S streams
+                # (each waits for the previous), so the library still sees S streams
+                e0.record(stream)
+                prev = stream
+                for i in range(n1):
+                    h = i % S
+                    streams[h].wait_stream(prev)
+                    run(after + n1 + i, streams[h], h)
+                    prev = streams[h]
+                stream.wait_stream(prev)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                single_ms = e0.elapsed_time(e1) / n1
+                res["launch_timing"] = f"one launch at a time, rotating over the {S} streams (keeps the in-flight tiling)"
+                launched_kernels()
     launch_ms = single_ms if single_ms is not None else kernel_ms
     fused = cfg["kind"] == "texture" and world == 1 and not args.loopback and args.texture_mode == "fused"
     if cfg["kind"] == "texture" and world == 1 and not args.loopback and not fused:
@@ -873,7 +893,10 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     got = dict(zip(keys, (float(v) for v in t)))
-    res["kernels"] = launched_kernels()  # every kernel instantiation this workload launched
+    # every kernel instantiation this workload launched (N = 1 with S > 1 streams: those of the
+    # timed frames)
+    res["kernels"] = res.pop("kernels_timed", None) or launched_kernels()
+    launched_kernels()
     if native:  # release the communicators on every rank at the same point (not at GC time)
         torch.cuda.synchronize(dev)
         dist.barrier()
@@ -1044,6 +1067,7 @@ def main():
         "settle": {"seconds": args.settle_s, "steps": m["settle_steps"]},
         **{k_: round(v, 4) for k_, v in parts.items()},
         **({"split": m["split"]} if m.get("split") else {}),
+        **({"launch_timing": m["launch_timing"]} if m.get("launch_timing") else {}),
         **({"halo_batch": m["halo_batch"]} if m.get("halo_batch") else {}),
         **({"weak": weak} if weak else {}),
     }

@@ -600,3 +600,38 @@ def test_launched_kernels_names_the_instantiation(dev, oracle):
     names = vip.launched_kernels()
     assert len(names) == 2 and any(n.startswith("void vip::texture_guide_fused_kernel<2, false>") for n in names)
     assert all("(" not in n for n in names)
+
+
+def test_small_frame_tiling_follows_frames_in_flight(dev, oracle):
+    """The plain kernel's small-frame tiling counts the frames in flight (distinct streams
+    among the device's last 8 launches): lenna-sized 512^2 frames on 4 streams take the
+    throughput tiling (16-wave 256-pixel tiles, 64 per frame: four frames side by side), one
+    stream the latency tiling (4-wave 256-pixel tiles). Same bytes either way."""
+    from various_image_processings_amd.filters import _BilateralImpl
+    torch = dev.torch_
+    img = oracle.random_image(512, 512)
+    src = dev.put(img)
+    want = oracle.bilateral(img, 11, threads=16)
+    impl = _BilateralImpl(512, 512, 11)
+    streams = [torch.cuda.Stream() for _ in range(4)]
+    outs = [dev.empty((512, 512, 3)) for _ in streams]
+    for _ in range(3):  # fill the ring with the 4 streams
+        for s, o in zip(streams, outs):
+            impl.bilateral_filter(src, o, stream=s)
+    torch.cuda.synchronize()
+    vip.launched_kernels()
+    for _ in range(2):
+        for s, o in zip(streams, outs):
+            impl.bilateral_filter(src, o, stream=s)
+    torch.cuda.synchronize()
+    assert vip.launched_kernels() == ["void vip::bilateral_kernel<5, 16, false, true, 32, 4, 768, false, 64, false>"]
+    for o in outs:
+        assert np.array_equal(dev.get(o), want)
+    for _ in range(8):  # one stream only: the ring forgets the others
+        impl.bilateral_filter(src, outs[0], stream=streams[0])
+    torch.cuda.synchronize()
+    vip.launched_kernels()
+    impl.bilateral_filter(src, outs[1], stream=streams[0])
+    torch.cuda.synchronize()
+    assert vip.launched_kernels() == ["void vip::bilateral_kernel<5, 4, false, true, 32, 4, 768, false, 64, false>"]
+    assert np.array_equal(dev.get(outs[0]), want) and np.array_equal(dev.get(outs[1]), want)

@@ -273,10 +273,16 @@ struct Tiling {
     int waves;
     bool wide;
 };
-inline Tiling small_frame_tiling(int width, int out_rows) {
+// With F frames in flight (distinct streams among the device's recent launches,
+// vip_capi.hip frames_in_flight) the frames share the chip, so a frame's rounds are counted
+// on cus / F CUs: a small frame then takes the tiling that fills its share, not the one
+// that ends soonest alone (C1 with 4 streams: 16-wave 256-px tiles, 61.8k against 27.3k
+// Mpx/s for the one-frame choice, profiles/r03 small-frame tables in DESIGN.md section 4).
+inline Tiling small_frame_tiling(int width, int out_rows, int inflight = 1) {
     const int forced = bilateral_forced_waves();
     const int fwide = bilateral_forced_wide();  // 0 auto, 1 narrow, 2 wide
-    const int cus = device_cus();
+    const int share = device_cus() / (inflight > 1 ? inflight : 1);  // CUs per frame
+    const int cus = share > 0 ? share : 1;
     const int cand[3] = {16, 8, 4};
     const float cost[3] = {1.0f, 1.25f, 1.8f};
     Tiling best{16, false};
@@ -333,7 +339,7 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
             return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
 #endif
         if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
-            const Tiling t = small_frame_tiling(a.width, a.out_rows);
+            const Tiling t = small_frame_tiling(a.width, a.out_rows, a.inflight);
             if (t.wide) {
                 if (t.waves == 16) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
                 if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8, true>(a, stream);
@@ -377,7 +383,8 @@ template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     if constexpr (!JOINT && VIP_BIL_SAT) {  // plain filter, 128-pixel 16-wave tiles: 512 x 32 LUT (SatLut)
         if (a.lut_nonzero <= 511) {
-            const Tiling t = R <= VIP_BIL_SMALL_MAX_R ? small_frame_tiling(a.width, a.out_rows) : Tiling{16, false};
+            const Tiling t = R <= VIP_BIL_SMALL_MAX_R ? small_frame_tiling(a.width, a.out_rows, a.inflight)
+                                                      : Tiling{16, false};
             if (t.waves == 16 && !t.wide) return launch_bilateral_ne<R, JOINT, FMA, 768, false, true>(a, stream);
         }
     }

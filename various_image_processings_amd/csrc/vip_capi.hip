@@ -6,6 +6,7 @@
 // LUTs once per handle, own device scratch, validate arguments. Unlike the
 // reference, run functions are asynchronous on the caller's stream and return a
 // status instead of printing it.
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -156,7 +157,33 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.color = d_color;
     a.lut_nonzero = lut_nonzero;
     a.fold = d_fold;
+    a.inflight = 1;
     std::memcpy(a.ws, wsq, sizeof(a.ws));
+}
+
+// Frames in flight on the current device, for the plain bilateral kernel's small-frame
+// tiling: the distinct streams among the device's last 8 plain-bilateral launches, at most
+// 4 (the hardware queues a process gets by default, GPU_MAX_HW_QUEUES). One stream (or
+// launches that alternate streams one at a time) counts 1. The choice changes the tiling
+// only, never the bytes.
+static int frames_in_flight(hipStream_t s) {
+    constexpr int kDevs = 16, kRing = 8;
+    static std::atomic<uintptr_t> recent[kDevs][kRing];
+    static std::atomic<unsigned> pos[kDevs];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    dev &= kDevs - 1;
+    recent[dev][pos[dev].fetch_add(1, std::memory_order_relaxed) % kRing].store((uintptr_t)s + 1,
+                                                                                 std::memory_order_relaxed);
+    uintptr_t seen[kRing];
+    int n = 0;
+    for (int i = 0; i < kRing; ++i) {
+        const uintptr_t v = recent[dev][i].load(std::memory_order_relaxed);
+        bool dup = v == 0;
+        for (int j = 0; j < n && !dup; ++j) dup = seen[j] == v;
+        if (!dup) seen[n++] = v;
+    }
+    return n < 1 ? 1 : (n > 4 ? 4 : n);
 }
 
 // vip_bilateral_set_waves: one process-wide value, read by every bilateral launcher
@@ -443,6 +470,7 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
     fill_args(a, h->width, d_src, src_pitch, joint ? d_guide : d_src, joint ? guide_pitch : src_pitch, d_dst,
               dst_pitch, out_rows, src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, joint ? h->d_fold : nullptr,
               h->wsq);
+    if (!joint) a.inflight = frames_in_flight((hipStream_t)stream);
     return launch_bilateral(h->radius, joint, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
 }
 

@@ -85,6 +85,7 @@ struct StencilArgs {
     const float* color;    // colour LUT in device memory
     int lut_nonzero;       // entries [lut_nonzero, end) of the colour LUT are exactly 0
     const float* fold;     // or null: [disc_r2_count(R)][kFoldEntries] = RN(ws(r^2) * colour[d])
+    int inflight;          // host only: frames in flight on this device (the small-frame tiling's model)
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 
