@@ -623,7 +623,7 @@ static int run_graph(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
         if (g.slab == slab && g.out == out && g.pitch == out_pitch && g.stream == s)
             return (int)hipGraphLaunch(g.exec, s);
     if (h->graphs.size() >= kMaxGraphs) {
-        VIP_HIP_TRY(hipStreamSynchronize(s));  // the oldest graph may still be in flight on s
+        VIP_HIP_TRY(hipStreamSynchronize(h->graphs.front().stream));  // the oldest graph may still be in flight
         (void)hipGraphExecDestroy(h->graphs.front().exec);
         h->graphs.erase(h->graphs.begin());
     }
