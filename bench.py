@@ -800,6 +800,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         dist.barrier()
     torch.cuda.synchronize(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    launched_kernels()  # the line names the kernels of the timed steps (not of the settle's first launches)
     t0 = time.perf_counter()
     ev0.record(stream)
     for s in streams[1:]:
@@ -809,6 +810,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     if native:
         flush()  # a partial last batch is part of the timed frames
     host_s = time.perf_counter() - t0  # every step enqueued
+    res["kernels_timed"] = launched_kernels()
     for s in streams[1:]:
         stream.wait_stream(s)
     ev1.record(stream)
@@ -843,8 +845,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             # frames on ONE stream, back to back, after the timed region (the S-stream
             # launches overlap, so their event spans are not launch durations)
             n1 = max(4, args.steps // 4)
-            timed_kernels = set(launched_kernels())
-            res["kernels_timed"] = sorted(timed_kernels)
+            timed_kernels = set(res["kernels_timed"])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
             for i in range(n1):
@@ -857,9 +858,12 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
                 # did (its small-frame tiling counts the streams in use): time the timed
                 # region's kernel instead, one launch at a time but rotating over the S streams
                 # (each waits for the previous), so the library still sees S streams
-                e0.record(stream)
                 prev = stream
-                for i in range(n1):
+                for i in range(n1 + 8):  # the first 8 (untimed) refill the library's stream history
+                    if i == 8:
+                        prev.synchronize()
+                        e0.record(stream)
+                        prev = stream
                     h = i % S
                     streams[h].wait_stream(prev)
                     run(after + n1 + i, streams[h], h)
@@ -895,7 +899,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     got = dict(zip(keys, (float(v) for v in t)))
     # every kernel instantiation this workload launched (N = 1 with S > 1 streams: those of the
     # timed frames)
-    res["kernels"] = res.pop("kernels_timed", None) or launched_kernels()
+    res["kernels"] = res.pop("kernels_timed")
     launched_kernels()
     if native:  # release the communicators on every rank at the same point (not at GC time)
         torch.cuda.synchronize(dev)
