@@ -141,6 +141,12 @@ int vip_bilateral_set_waves(int waves);
  * variable VIP_BIL_WIDE sets the initial value. A forced wave count with mode 0 keeps
  * 128-pixel tiles. */
 int vip_bilateral_set_wide(int mode);
+/* Frames in flight the same choice plans for: 0 (default) = counted per device from the
+ * distinct streams among its last 8 plain-bilateral launches (at most 4), so frames in
+ * flight on several streams each get a tiling sized for their share of the CUs; 1..4 forces
+ * the count (a measurement knob: e.g. timing one frame alone with the tiling the in-flight
+ * frames use). Results are identical for every setting. */
+int vip_bilateral_set_frames_in_flight(int n);
 
 /* ---- adaptive bilateral: CudaAdaptiveBilateralFilter
  *      (include/cuda/adaptive_bilateral_filter.hpp:9-19, src/adaptive_bilateral_filter_impl.cu:117-191) ---- */

@@ -27,6 +27,7 @@ from .filters import (  # noqa: F401
     device_synchronize,
     launched_kernels,
     max_ksize,
+    set_bilateral_frames_in_flight,
     set_bilateral_waves,
     set_bilateral_wide,
     set_stencil_path,

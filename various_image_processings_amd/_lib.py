@@ -79,6 +79,7 @@ SIGNATURES = {
     "vip_texture_set_mode": (_c_int, [_c_void_p, _c_int]),
     "vip_bilateral_set_waves": (_c_int, [_c_int]),
     "vip_bilateral_set_wide": (_c_int, [_c_int]),
+    "vip_bilateral_set_frames_in_flight": (_c_int, [_c_int]),
     "vip_texture_iterate_rows": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_int, _c_int, _c_int,
                                           _c_void_p]),
     "vip_texture_blur_rtv": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),

@@ -166,6 +166,7 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
 // 4 (the hardware queues a process gets by default, GPU_MAX_HW_QUEUES). One stream (or
 // launches that alternate streams one at a time) counts 1. The choice changes the tiling
 // only, never the bytes.
+static std::atomic<int> g_bil_inflight{0};  // vip_bilateral_set_frames_in_flight: 0 = counted
 static int frames_in_flight(hipStream_t s) {
     constexpr int kDevs = 16, kRing = 8;
     static std::atomic<uintptr_t> recent[kDevs][kRing];
@@ -183,6 +184,8 @@ static int frames_in_flight(hipStream_t s) {
         for (int j = 0; j < n && !dup; ++j) dup = seen[j] == v;
         if (!dup) seen[n++] = v;
     }
+    const int forced = g_bil_inflight.load(std::memory_order_relaxed);
+    if (forced) return forced;
     return n < 1 ? 1 : (n > 4 ? 4 : n);
 }
 
@@ -330,6 +333,12 @@ int vip_bilateral_set_waves(int waves) {
 int vip_bilateral_set_wide(int mode) {
     if (mode < 0 || mode > 2) return VIP_ERR_INVALID_ARGUMENT;
     g_bil_wide.store(mode, std::memory_order_relaxed);
+    return 0;
+}
+
+int vip_bilateral_set_frames_in_flight(int n) {
+    if (n < 0 || n > 4) return VIP_ERR_INVALID_ARGUMENT;
+    g_bil_inflight.store(n, std::memory_order_relaxed);
     return 0;
 }
 

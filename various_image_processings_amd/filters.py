@@ -29,7 +29,7 @@ from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
 __all__ = [
     "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
     "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
-    "set_bilateral_waves", "set_bilateral_wide", "launched_kernels", "set_stencil_path", "max_ksize",
+    "set_bilateral_waves", "set_bilateral_wide", "set_bilateral_frames_in_flight", "launched_kernels", "set_stencil_path", "max_ksize",
 ]
 
 
@@ -97,6 +97,12 @@ def set_bilateral_wide(mode: int = 0) -> None:
     per launch, 1 = 128-pixel tiles (8 outputs per thread), 2 = 256-pixel tiles (one row
     per wave, 4 outputs per thread). Outputs are identical for every setting."""
     call("vip_bilateral_set_wide", int(mode))
+
+
+def set_bilateral_frames_in_flight(n: int = 0) -> None:
+    """include/vip.h vip_bilateral_set_frames_in_flight: 0 = counted from the streams in use
+    (default), 1..4 forced. A measurement knob; results are identical for every setting."""
+    call("vip_bilateral_set_frames_in_flight", int(n))
 
 
 def launched_kernels() -> list:
