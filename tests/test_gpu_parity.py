@@ -635,3 +635,13 @@ def test_small_frame_tiling_follows_frames_in_flight(dev, oracle):
     torch.cuda.synchronize()
     assert vip.launched_kernels() == ["void vip::bilateral_kernel<5, 4, false, true, 32, 4, 768, false, 64, false>"]
     assert np.array_equal(dev.get(outs[0]), want) and np.array_equal(dev.get(outs[1]), want)
+    vip.set_bilateral_frames_in_flight(4)  # the measurement override: one stream, the in-flight tiling
+    try:
+        impl.bilateral_filter(src, outs[2], stream=streams[0])
+        torch.cuda.synchronize()
+    finally:
+        vip.set_bilateral_frames_in_flight(0)
+    assert vip.launched_kernels() == ["void vip::bilateral_kernel<5, 16, false, true, 32, 4, 768, false, 64, false>"]
+    assert np.array_equal(dev.get(outs[2]), want)
+    with pytest.raises(vip.VipError):
+        vip.set_bilateral_frames_in_flight(5)
