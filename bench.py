@@ -80,15 +80,39 @@ def launch_ranks(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script
     status); 124 when the whole run exceeds timeout_s, after its process group -- the
     launcher and every rank it started -- has been terminated (SIGTERM, then SIGKILL after
     10 s)."""
+    return _run_ranks(n, argv, timeout_s, script, capture=False)[0]
+
+
+def launch_ranks_json(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script: str | None = None):
+    """launch_ranks, but the ranks' JSON lines are collected instead of printed (every other
+    stdout line is passed through): (exit status, [JSON lines])."""
+    return _run_ranks(n, argv, timeout_s, script, capture=True)
+
+
+def _run_ranks(n, argv, timeout_s, script, capture):
     import signal
     import subprocess
+    import threading
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # the host driver supports dmabuf IPC only
     cmd = rank_launch_argv(n, argv, free_port(), script)
     print(f"bench.py: --gpus {n}: starting {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
-    proc = subprocess.Popen(cmd, env=env, start_new_session=True)
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True, stdout=subprocess.PIPE if capture else None,
+                            text=True, bufsize=1)
+    lines = []
+    reader = None
+    if capture:
+        def pump():
+            for line in proc.stdout:
+                if line.lstrip().startswith("{"):
+                    lines.append(line.strip())
+                else:
+                    sys.stdout.write(line)
+                    sys.stdout.flush()
+        reader = threading.Thread(target=pump, daemon=True)
+        reader.start()
     try:
-        return proc.wait(timeout=timeout_s)
+        rc = proc.wait(timeout=timeout_s)
     except subprocess.TimeoutExpired:
         print(f"bench.py: the {n}-rank run did not finish in {timeout_s:.0f} s; terminating it", file=sys.stderr,
               flush=True)
@@ -102,7 +126,36 @@ def launch_ranks(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script
                 break
             except subprocess.TimeoutExpired:
                 continue
-        return 124
+        rc = 124
+    if reader is not None:
+        reader.join(timeout=10)
+    return rc, lines
+
+
+GRAPH_ATTEMPT_TIMEOUT_S = 420.0
+
+
+def launch_with_graph_attempt(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script: str | None = None) -> int:
+    """`python bench.py --gpus N` (native exchange): first the run whose split / batch trial
+    also times each frame replayed from a captured hipGraph (--graph: the image's HIP + RCCL
+    loaded before torch, preload_system_rocm); if that run fails or runs out of its own
+    bound, the same measurement without graph capture (--no-graph). Exactly one JSON line
+    is printed, the last one of the run that succeeded, with `graph_attempt` saying what
+    happened. Returns the exit status of the run whose line was printed."""
+    rc, lines = launch_ranks_json(n, list(argv) + ["--graph"], min(timeout_s, GRAPH_ATTEMPT_TIMEOUT_S), script)
+    if rc == 0 and lines:
+        line = json.loads(lines[-1])
+        line["graph_attempt"] = "ok: the trial included the captured form"
+        print(json.dumps(line), flush=True)
+        return 0
+    why = f"the run with graph capture ended with status {rc}" + ("" if lines else " and no line")
+    print(f"bench.py: {why}; measuring again without graph capture", file=sys.stderr, flush=True)
+    rc2, lines2 = launch_ranks_json(n, list(argv) + ["--no-graph"], timeout_s, script)
+    if lines2:
+        line = json.loads(lines2[-1])
+        line["graph_attempt"] = f"failed ({why}); measured without graph capture"
+        print(json.dumps(line), flush=True)
+    return rc2
 
 
 SYSTEM_ROCM = ("/opt/rocm/lib/libamdhip64.so.7", "/opt/rocm/lib/librccl.so.1")
@@ -221,7 +274,9 @@ def parse():
     # N > 1 native: also time each frame replayed from a captured hipGraph (vip_shard_set_graph)
     # in the split / batch trial; loads the image's HIP runtime and RCCL before torch
     # (preload_system_rocm)
-    p.add_argument("--graph", action=argparse.BooleanOptionalAction, default=False)
+    # default: off inside a rank; `python bench.py --gpus N` (native exchange) first tries a
+    # run with it and falls back to one without (launch_with_graph_attempt)
+    p.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None)
     # --gpus N > 1 without WORLD_SIZE in the environment: this process starts the N ranks
     # itself (a child torchrun) and ends them after this many seconds
     p.add_argument("--launch-timeout", type=float, default=LAUNCH_TIMEOUT_S)
@@ -917,6 +972,9 @@ def main():
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.rehearse_native:
         # plain `python bench.py --gpus N`: start the N ranks (nothing has touched the GPU)
+        native = args.exchange in (None, "native") and not args.same_device and args.backend != "gloo"
+        if args.graph is None and native:
+            sys.exit(launch_with_graph_attempt(args.gpus, sys.argv[1:], args.launch_timeout))
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
     if args.graph:
         preload_system_rocm()

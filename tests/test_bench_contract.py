@@ -193,3 +193,32 @@ def test_bench_gpus_2_from_a_plain_shell_launches_ranks():
     assert "starting 2 ranks" in r.stderr
     assert "torch.distributed.run" in r.stderr
     assert r.returncode not in (0, 124)
+
+
+GRAPH_PROBE = r'''
+import json, os, sys
+graph = "--graph" in sys.argv
+if graph and sys.argv[1] == "crash":
+    sys.exit(7)
+print("rank", os.environ["RANK"], "says hello", flush=True)
+if os.environ["RANK"] == "0":
+    print(json.dumps({"metric": "m", "value": 2.0 if graph else 1.0}), flush=True)
+'''
+
+
+@pytest.mark.parametrize("mode", ["ok", "crash"])
+def test_launch_with_graph_attempt_prints_one_line(tmp_path, mode, capfd):
+    """`python bench.py --gpus N` (native exchange, no --graph/--no-graph): a first run with
+    graph capture; when it fails, the same run without it. Exactly one JSON line either way,
+    saying which run it came from; other stdout lines pass through."""
+    script = tmp_path / "gprobe.py"
+    script.write_text(GRAPH_PROBE)
+    rc = bench.launch_with_graph_attempt(2, [mode], timeout_s=120, script=str(script))
+    out = capfd.readouterr().out
+    lines = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
+    assert rc == 0 and len(lines) == 1
+    assert "says hello" in out
+    if mode == "ok":
+        assert lines[0]["value"] == 2.0 and lines[0]["graph_attempt"].startswith("ok")
+    else:
+        assert lines[0]["value"] == 1.0 and lines[0]["graph_attempt"].startswith("failed (the run with graph")
