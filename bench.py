@@ -179,6 +179,29 @@ def halo_batches(streams: int) -> list:
     i % NBUF to always meet the same stream (its halo receive then stays ordered after its
     last reader)."""
     return [b for b in (1, 2, 3) if NBUF % (b * streams) == 0]
+
+
+# N > 1 native: frames in flight the trial may use when neither --streams nor the config
+# fixes it. A rank's frame is a slab (C2 at N = 8: 270 rows, ~25 us), so a stream's
+# exchange latency is about one filter launch; more streams keep the chip fed while the
+# halos of the others are in flight (and the small-slab tiling counts them, share = CUs / S).
+TRIAL_STREAMS = (2, 3, 4)
+
+
+def native_forms(stream_counts, texture: bool, graph: bool) -> list:
+    """The N > 1 native trial's forms (S streams, split, B frames per RCCL group, graph,
+    shared launches): every S with each B that keeps a buffer on one stream (halo_batches),
+    the split / one-launch pair (the texture filter has no split), with `graph` one captured
+    form per (S, split), and for B > 1 after the exchange the B frames in shared launches
+    (vip_shard_set_frames_launch; plain and adaptive filters)."""
+    forms = []
+    for n in stream_counts:
+        for split in ((False,) if texture else (True, False)):
+            forms += [(n, split, b, False, False) for b in halo_batches(n)]
+            forms += [(n, split, 1, True, False)] if graph else []
+            if not split and not texture:
+                forms += [(n, split, b, False, True) for b in halo_batches(n) if b > 1]
+    return forms
 BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
 
 
@@ -252,7 +275,7 @@ def parse():
     # 0.178 -> 0.173 ms, C3 0.327 -> 0.323, C4 0.717 -> 0.641 ms per frame with 2; 3 no
     # better. S must divide the 12 rotating buffers (a buffer always meets the same stream)
     p.add_argument("--streams", type=int, default=None, choices=[1, 2, 3, 4, 6],
-                   help="default: the config's own (c1 4), else 2")
+                   help="default: the config's own (c1 4), else 2; N > 1 native: the trial picks 2, 3 or 4")
     # N>1: "strong" splits the metric's frame (C2/C3: 3840x2160) over the ranks (default
     # for c2, c3, c5), "weak" gives every rank a 2160-row slab of an (N*2160)-row frame
     # (default for c4). A strong c2/c3 line also carries the weak figure ("weak" key)
@@ -610,9 +633,11 @@ def native_shards(args, cfg, frame_h, rank, world, n):
     return shards, None
 
 
-def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
+def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms=None):
     """Build one workload (buffers, handles) and time it: W warm-up steps, then K steps
-    between barriers + device syncs, max over ranks. Returns the measured quantities."""
+    between barriers + device syncs, max over ranks. Returns the measured quantities.
+    s_forms: the stream counts the N > 1 native trial may pick from (at most len(streams));
+    default: all the streams."""
     import torch.distributed as dist
 
     from various_image_processings_amd.filters import _TextureImpl, launched_kernels
@@ -712,18 +737,19 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
     # group's cost is mostly fixed, profiles/r03_rccl_enqueue.txt). Frame i then runs on
     # stream (i // B) % S; B * S divides NBUF, so buffer i % NBUF still always meets the
     # same stream and a halo receive into it stays ordered after its last reader.
-    hb = dict(B=1, pending=[])
+    s_forms = list(s_forms or [S])
+    hb = dict(B=1, S=s_forms[0], pending=[])  # S: the streams in use (the trial may change it)
 
     def flush():
         if hb["pending"]:
-            h = (hb["pending"][0] // hb["B"]) % S
+            h = (hb["pending"][0] // hb["B"]) % hb["S"]
             nbatches[h]([sp[j % NBUF] for j in hb["pending"]], [dp[j % NBUF] for j in hb["pending"]], sraw[h])
             hb["pending"].clear()
 
     def step(i, sample=False):
         # step i on stream i % S; buffer i % NBUF therefore always meets the same stream
         # (S divides NBUF), so a halo receive into it is ordered after its last reader
-        h = 0 if sample else i % S
+        h = 0 if sample else i % hb["S"]
         s = streams[h]
         if native and not sample and hb["B"] > 1:
             # batches end on multiples of B (a phase end flushes a partial one), so every
@@ -798,17 +824,16 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
         # (buffer, stream)'s exchange + launches with one hipGraphLaunch: the per-frame host
         # cost of an RCCL group (16-30 us, profiles/r03_rccl_enqueue.txt) against a rank's
         # ~25 us C2 launch at N = 8 is what it removes.
+        # With several stream counts (TRIAL_STREAMS), S is a trial dimension too: frames in
+        # flight hide one stream's exchange latency behind the others' launches.
         trial = {}
         n_trial = 42  # a multiple of every B
-        batches = halo_batches(S)
-        forms = []
-        for split in ((False,) if cfg["kind"] == "texture" else (True, False)):
-            forms += [(split, b, False) for b in batches] + ([(split, 1, True)] if args.graph else [])
-        for split, b, graph in forms:
+        for n_s, split, b, graph, shared in native_forms(s_forms, cfg["kind"] == "texture", bool(args.graph)):
             for x in shards:
                 x.set_split(split)
                 x.set_graph(graph)
-            hb["B"] = b
+                x.set_frames_launch(shared)
+            hb["B"], hb["S"] = b, n_s
             for _ in range(NBUF):  # untimed: captures every (buffer, stream) graph in graph mode
                 step(i_settle)
                 i_settle += 1
@@ -824,25 +849,30 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state):
             dist.barrier()
             dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            trial[(split, b, graph)] = float(dt[0])
-        best_split, best_b, best_graph = min(trial, key=trial.get)
+            trial[(n_s, split, b, graph, shared)] = float(dt[0])
+        best_s, best_split, best_b, best_graph, best_shared = min(trial, key=trial.get)
         res["split_on"] = best_split
         for x in shards:
             x.set_split(best_split)
             x.set_graph(best_graph)
-        hb["B"] = best_b
+            x.set_frames_launch(best_shared)
+        hb["B"], hb["S"] = best_b, best_s
+        res["streams"] = best_s
         res["exchange"] += ("; interior rows overlapped with the exchange, then the edge bands" if best_split
                             else "; one launch over the own rows after the exchange")
         if best_b > 1:
             res["exchange"] += f"; the halos of {best_b} frames per RCCL group"
+            if best_shared:
+                res["exchange"] += ", filtered in one launch"
         if best_graph:
             res["exchange"] += "; each frame replayed from a captured hipGraph"
         res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best_split
                             else "one launch after the exchange",
-                            graph=best_graph,
-                            trial_ms_per_step={("split" if sp_ else "one_launch") + (f"_batch{b_}" if b_ > 1 else "")
-                                               + ("_graph" if g_ else ""): round(v, 4)
-                                               for (sp_, b_, g_), v in trial.items()})
+                            graph=best_graph, frames_launch=best_shared,
+                            trial_ms_per_step={(f"s{s_}_" if len(s_forms) > 1 else "")
+                                               + ("split" if sp_ else "one_launch") + (f"_batch{b_}" if b_ > 1 else "")
+                                               + ("_graph" if g_ else "") + ("_one_kernel" if sh_ else ""): round(v, 4)
+                                               for (s_, sp_, b_, g_, sh_), v in trial.items()})
         res["halo_batch"] = best_b
     res["settle_steps"] = i_settle
     base = i_settle
@@ -1016,7 +1046,8 @@ def main():
 
     import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
 
-    S = args.streams = args.streams or cfg.get("streams", 2)
+    fixed_streams = args.streams or cfg.get("streams")
+    S = args.streams = fixed_streams or 2
     if "tiling" in cfg and world == 1:  # the config's tile shape (include/vip.h tuning knobs)
         vip.set_bilateral_waves(cfg["tiling"][0])
         vip.set_bilateral_wide(cfg["tiling"][1])
@@ -1037,12 +1068,18 @@ def main():
     gw = args.loopback if args.loopback > 1 else world  # ranks of the row split (geometry)
     sharded = gw > 1  # this process filters a slab of a larger frame
     frame_h = cfg.get("frame_height") or (per_rank * gw if args.scaling == "weak" else per_rank)
-    m = measure(args, cfg, frame_h, torch, dev, rank, world, streams, state)
+    s_forms = None
+    if sharded and args.exchange == "native" and not fixed_streams:
+        # N > 1 native: the trial also picks the frames in flight (TRIAL_STREAMS), one
+        # shard per stream
+        s_forms = list(TRIAL_STREAMS)
+        streams += [torch.cuda.Stream(dev) for _ in range(max(s_forms) - len(streams))]
+    m = measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms)
     weak = None
     if world > 1 and args.scaling == "strong" and per_rank and not args.no_weak:
         # the weak-scaling figure beside it: a full 2160-row slab per rank of an
         # (N*2160)x3840 frame
-        wm = measure(args, cfg, per_rank * world, torch, dev, rank, world, streams, state)
+        wm = measure(args, cfg, per_rank * world, torch, dev, rank, world, streams, state, s_forms)
         wpx = wm["rows"] * cfg["width"] * world
         weak = dict(value=round(wpx / (wm["elapsed"] / args.steps) / 1e6, 2),
                     ms_per_step=round(wm["elapsed"] / args.steps * 1e3, 4), frame=f"{cfg['width']}x{per_rank * world}",
@@ -1123,7 +1160,7 @@ def main():
         "kernel_ms": round(launch_ms, 4),
         # frames in flight on S streams (step i on stream i % S); at N=1 and S>1 the
         # timed region's device time per frame, all streams together
-        "streams": S,
+        "streams": m.get("streams", S),
         **({"frame_ms_in_flight": round(m["frame_ms"], 4)} if world == 1 and S > 1 else {}),
         "settle": {"seconds": args.settle_s, "steps": m["settle_steps"]},
         **{k_: round(v, 4) for k_, v in parts.items()},

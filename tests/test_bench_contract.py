@@ -222,3 +222,20 @@ def test_launch_with_graph_attempt_prints_one_line(tmp_path, mode, capfd):
         assert lines[0]["value"] == 2.0 and lines[0]["graph_attempt"].startswith("ok")
     else:
         assert lines[0]["value"] == 1.0 and lines[0]["graph_attempt"].startswith("failed (the run with graph")
+
+
+def test_native_trial_forms_keep_buffers_on_one_stream():
+    """The N > 1 native trial's forms (streams S, split, frames per RCCL group B, graph):
+    every S of TRIAL_STREAMS appears, each (S, B) keeps buffer i % NBUF on one stream, the
+    texture filter has no split form, and graph forms appear only when asked for."""
+    forms = bench.native_forms(bench.TRIAL_STREAMS, texture=False, graph=False)
+    assert {f[0] for f in forms} == set(bench.TRIAL_STREAMS)
+    assert all(bench.NBUF % (s * b) == 0 and not g for s, _, b, g, _ in forms)
+    assert {(s, sp) for s, sp, _, _, _ in forms} == {(s, sp) for s in bench.TRIAL_STREAMS for sp in (True, False)}
+    # shared launches: only after the exchange (no split) and for more than one frame
+    assert all(not sp and b > 1 for _, sp, b, _, sh in forms if sh)
+    assert {(s, b) for s, _, b, _, sh in forms if sh} == {(s, b) for s in bench.TRIAL_STREAMS
+                                                         for b in bench.halo_batches(s) if b > 1}
+    tex = bench.native_forms([2], texture=True, graph=True)
+    assert all(not sp and not sh for _, sp, _, _, sh in tex) and [f for f in tex if f[3]] == [(2, False, 1, True, False)]
+    assert len(set(forms)) == len(forms)

@@ -87,21 +87,22 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     TilePrefetch<R, ROWS, NT, P> pf;
     LutStage<NT, NE, COPIES> ls;  // LUT reads go out before the first tile's
     ls.load(a.color);
-    {
-        const int mt = xcd_tile(tile, a.tiles_total);
-        pf.issue(a.src, a.src_pitch, a, (mt % a.tiles_x) * G::TW, (mt / a.tiles_x) * TH);
+    {  // multi-frame launches: frame f's tiles follow frame f - 1's
+        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        pf.issue(frame_ptr(a.fsrc, a.src, ft.f), a.src_pitch, a, (ft.t % a.tiles_x) * G::TW, (ft.t / a.tiles_x) * TH);
     }
     ls.store(lut);
     pf.commit(plane);
     __syncthreads();
 
     while (true) {
-        const int mt = xcd_tile(tile, a.tiles_total);
-        const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
+        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
         if (next < a.tiles_total) {
-            const int mn = xcd_tile(next, a.tiles_total);
-            pf.issue(a.src, a.src_pitch, a, (mn % a.tiles_x) * G::TW, (mn / a.tiles_x) * TH);
+            const FrameTile fn = frame_tile(a, xcd_tile(next, a.tiles_total));
+            pf.issue(frame_ptr(a.fsrc, a.src, fn.f), a.src_pitch, a, (fn.t % a.tiles_x) * G::TW,
+                     (fn.t / a.tiles_x) * TH);
         }
         if constexpr (VBOX) {
             // ---- pass 1a (whole workgroup): vertical K-row sums, 4 output rows per run ----
@@ -290,7 +291,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
 
             uint32_t o[P];
             finish_outputs(a01, a2k, o);
-            store_px(a, ty0 + ty, tx0 + tx * P, o);
+            store_px_to(a, frame_ptr(a.fdst, a.dst, ft.f), ty0 + ty, tx0 + tx * P, o);
         }
         if (next >= a.tiles_total) break;
         __syncthreads();
@@ -326,7 +327,8 @@ static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     note_launch(reinterpret_cast<const void*>(kern));
     StencilArgs args = a;
     args.tiles_x = (a.width + G::TW - 1) / G::TW;
-    args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);
+    args.tiles_frame = args.tiles_x * ((a.out_rows + TH - 1) / TH);
+    args.tiles_total = args.tiles_frame * (a.nframes < 1 ? 1 : a.nframes);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);

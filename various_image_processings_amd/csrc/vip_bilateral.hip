@@ -113,10 +113,12 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     // once per workgroup; its reads go out first
     std::conditional_t<SAT, SatStage<NT, SL>, LutStage<NT, NTAB * NE, COPIES>> ls;
     ls.load(FOLD ? a.fold : a.color);
+    // multi-frame launches (plain filter only: guide == src): frame f's tiles follow
+    // frame f - 1's, so a workgroup's next tile may be the next frame's
     {
-        const int mt = xcd_tile(tile, a.tiles_total);
-        const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
-        pg.issue(a.guide, a.guide_pitch, a, tx0, ty0);
+        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
+        pg.issue(JOINT ? a.guide : frame_ptr(a.fsrc, a.guide, ft.f), a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
     ls.store(SAT ? lds + SL::T / 4 : lut);
@@ -126,13 +128,13 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
 
     for ([[maybe_unused]] int it = 0;; ++it) {
         VIP_STAMP(it, 0);
-        const int mt = xcd_tile(tile, a.tiles_total);
-        const int tx0 = (mt % a.tiles_x) * G::TW, ty0 = (mt / a.tiles_x) * TH;
+        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
         if (next < a.tiles_total) {  // next tile's HBM reads fly under this tile's taps
-            const int mn = xcd_tile(next, a.tiles_total);
-            const int nx0 = (mn % a.tiles_x) * G::TW, ny0 = (mn / a.tiles_x) * TH;
-            pg.issue(a.guide, a.guide_pitch, a, nx0, ny0);
+            const FrameTile fn = frame_tile(a, xcd_tile(next, a.tiles_total));
+            const int nx0 = (fn.t % a.tiles_x) * G::TW, ny0 = (fn.t / a.tiles_x) * TH;
+            pg.issue(JOINT ? a.guide : frame_ptr(a.fsrc, a.guide, fn.f), a.guide_pitch, a, nx0, ny0);
             if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
         }
         if (ty0 + wave * G::RPW < a.out_rows) {  // wave-uniform: skip rows past the frame
@@ -182,7 +184,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
 
             uint32_t o[P];
             finish_outputs<P, VIP_BIL_RCP != 0>(a01, a2k, o);
-            store_px(a, ty0 + ty, tx0 + tx * P, o);
+            store_px_to(a, JOINT ? a.dst : frame_ptr(a.fdst, a.dst, ft.f), ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);
         if (next >= a.tiles_total) {
@@ -278,7 +280,7 @@ struct Tiling {
 // on cus / F CUs: a small frame then takes the tiling that fills its share, not the one
 // that ends soonest alone (C1 with 4 streams: 16-wave 256-px tiles, 61.8k against 27.3k
 // Mpx/s for the one-frame choice, profiles/r03 small-frame tables in DESIGN.md section 4).
-inline Tiling small_frame_tiling(int width, int out_rows, int inflight = 1) {
+inline Tiling small_frame_tiling(int width, int out_rows, int inflight = 1, int nframes = 1) {
     const int forced = bilateral_forced_waves();
     const int fwide = bilateral_forced_wide();  // 0 auto, 1 narrow, 2 wide
     const int share = device_cus() / (inflight > 1 ? inflight : 1);  // CUs per frame
@@ -295,7 +297,7 @@ inline Tiling small_frame_tiling(int width, int out_rows, int inflight = 1) {
         for (int i = 0; i < 3; ++i) {
             if (forced && cand[i] != forced) continue;
             const int th = cand[i] * rpw;
-            const long long tiles = tiles_x * ((out_rows + th - 1) / th);
+            const long long tiles = tiles_x * ((out_rows + th - 1) / th) * (nframes > 1 ? nframes : 1);
             const float t = (float)((tiles + cus - 1) / cus) * cand[i] * cost[i] * (wide ? VIP_BIL_WIDE_WORK : 1.f);
             if (first || t < best_t) best = Tiling{cand[i], wide != 0}, best_t = t, first = false;
         }
@@ -339,7 +341,7 @@ static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
             return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
 #endif
         if constexpr (!JOINT && !FOLD && NE == 768 && WAVES == 16 && R <= VIP_BIL_SMALL_MAX_R) {
-            const Tiling t = small_frame_tiling(a.width, a.out_rows, a.inflight);
+            const Tiling t = small_frame_tiling(a.width, a.out_rows, a.inflight, a.nframes);
             if (t.wide) {
                 if (t.waves == 16) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 16, true>(a, stream);
                 if (t.waves == 8) return launch_bilateral_w<R, JOINT, FMA, NE, FOLD, 8, true>(a, stream);
@@ -372,7 +374,8 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     note_launch(reinterpret_cast<const void*>(kern));
     StencilArgs args = a;
     args.tiles_x = (a.width + G::TW - 1) / G::TW;
-    args.tiles_total = args.tiles_x * ((a.out_rows + TH - 1) / TH);
+    args.tiles_frame = args.tiles_x * ((a.out_rows + TH - 1) / TH);
+    args.tiles_total = args.tiles_frame * (JOINT || a.nframes < 1 ? 1 : a.nframes);  // the joint filter: one frame
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
@@ -383,7 +386,7 @@ template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     if constexpr (!JOINT && VIP_BIL_SAT) {  // plain filter, 128-pixel 16-wave tiles: 512 x 32 LUT (SatLut)
         if (a.lut_nonzero <= 511) {
-            const Tiling t = R <= VIP_BIL_SMALL_MAX_R ? small_frame_tiling(a.width, a.out_rows, a.inflight)
+            const Tiling t = R <= VIP_BIL_SMALL_MAX_R ? small_frame_tiling(a.width, a.out_rows, a.inflight, a.nframes)
                                                       : Tiling{16, false};
             if (t.waves == 16 && !t.wide) return launch_bilateral_ne<R, JOINT, FMA, 768, false, true>(a, stream);
         }

@@ -158,6 +158,12 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.lut_nonzero = lut_nonzero;
     a.fold = d_fold;
     a.inflight = 1;
+    a.nframes = 1;
+    a.tiles_frame = 0;
+    for (int f = 0; f < kMaxBatchFrames; ++f) {
+        a.fsrc[f] = src;
+        a.fdst[f] = dst;
+    }
     std::memcpy(a.ws, wsq, sizeof(a.ws));
 }
 
@@ -483,6 +489,56 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
     return launch_bilateral(h->radius, joint, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
 }
 
+// Frames [f0, f0 + m) of a batch in one StencilArgs (m <= kMaxBatchFrames): frame 0's
+// pointers in src/dst, every frame's in fsrc/fdst; dword tile loads / qword stores only
+// when every frame allows them.
+static void fill_batch(StencilArgs& a, int m, const uint8_t* const* srcs, size_t src_pitch, uint8_t* const* dsts,
+                       size_t dst_pitch) {
+    a.nframes = m;
+    for (int f = 0; f < kMaxBatchFrames; ++f) {
+        a.fsrc[f] = srcs[f < m ? f : 0];
+        a.fdst[f] = dsts[f < m ? f : 0];
+        a.aligned = a.aligned && (uintptr_t)a.fsrc[f] % 4 == 0 && src_pitch % 4 == 0;
+        a.dst_aligned = a.dst_aligned && (uintptr_t)a.fdst[f] % 8 == 0 && dst_pitch % 8 == 0;
+    }
+}
+
+// Batch arguments: every pointer set, no output that is also an input of the batch.
+static int check_batch(int n, const uint8_t* const* srcs, uint8_t* const* dsts) {
+    if (n < 0 || (n > 0 && (!srcs || !dsts))) return VIP_ERR_INVALID_ARGUMENT;
+    for (int f = 0; f < n; ++f)
+        if (!srcs[f] || !dsts[f]) return VIP_ERR_INVALID_ARGUMENT;
+    for (int f = 0; f < n; ++f)
+        for (int g = 0; g < n; ++g)
+            if (dsts[f] == srcs[g]) return VIP_ERR_ALIASING;
+    return 0;
+}
+
+int vip_bilateral_run_rows_batch(vip_bilateral_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
+                                 uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
+                                 int row_hi, void* stream) {
+    if (!h || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+    if (const int rc = check_batch(n, d_srcs, d_dsts)) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    if (use_runtime_kernel(h->radius)) {  // the runtime-radius kernel: one launch per frame
+        for (int f = 0; f < n; ++f)
+            if (const int rc = vip_bilateral_run_rows(h, d_srcs[f], src_pitch, nullptr, 0, d_dsts[f], dst_pitch,
+                                                      out_rows, src_row0, row_lo, row_hi, stream))
+                return rc;
+        return 0;
+    }
+    for (int f0 = 0; f0 < n; f0 += kMaxBatchFrames) {
+        const int m = n - f0 < kMaxBatchFrames ? n - f0 : kMaxBatchFrames;
+        StencilArgs a;
+        fill_args(a, h->width, d_srcs[f0], src_pitch, d_srcs[f0], src_pitch, d_dsts[f0], dst_pitch, out_rows,
+                  src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, nullptr, h->wsq);
+        fill_batch(a, m, d_srcs + f0, src_pitch, d_dsts + f0, dst_pitch);
+        a.inflight = frames_in_flight(s);
+        if (const int rc = launch_bilateral(h->radius, false, h->numerics == VIP_NUMERICS_CUDA, a, s)) return rc;
+    }
+    return 0;
+}
+
 int vip_bilateral_run(vip_bilateral_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
                       void* stream) {
     if (!h) return VIP_ERR_INVALID_ARGUMENT;
@@ -543,6 +599,30 @@ int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pit
     fill_args(a, h->width, d_src, src_pitch, d_src, src_pitch, d_dst, dst_pitch, out_rows, src_row0, row_lo, row_hi,
               h->d_color, h->lut_nonzero, nullptr, h->wsq);
     return launch_adaptive(h->radius, h->numerics == VIP_NUMERICS_CUDA, a, (hipStream_t)stream);
+}
+
+int vip_adaptive_run_rows_batch(vip_adaptive_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
+                                uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
+                                int row_hi, void* stream) {
+    if (!h || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+    if (const int rc = check_batch(n, d_srcs, d_dsts)) return rc;
+    const hipStream_t s = (hipStream_t)stream;
+    if (use_runtime_kernel(h->radius)) {
+        for (int f = 0; f < n; ++f)
+            if (const int rc = vip_adaptive_run_rows(h, d_srcs[f], src_pitch, d_dsts[f], dst_pitch, out_rows, src_row0,
+                                                     row_lo, row_hi, stream))
+                return rc;
+        return 0;
+    }
+    for (int f0 = 0; f0 < n; f0 += kMaxBatchFrames) {
+        const int m = n - f0 < kMaxBatchFrames ? n - f0 : kMaxBatchFrames;
+        StencilArgs a;
+        fill_args(a, h->width, d_srcs[f0], src_pitch, d_srcs[f0], src_pitch, d_dsts[f0], dst_pitch, out_rows,
+                  src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, nullptr, h->wsq);
+        fill_batch(a, m, d_srcs + f0, src_pitch, d_dsts + f0, dst_pitch);
+        if (const int rc = launch_adaptive(h->radius, h->numerics == VIP_NUMERICS_CUDA, a, s)) return rc;
+    }
+    return 0;
 }
 
 int vip_adaptive_run(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,

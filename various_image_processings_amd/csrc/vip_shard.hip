@@ -114,6 +114,7 @@ struct vip_shard_s {
     ncclComm_t nccl = nullptr;   // VIP_SHARD_RCCL
     int peer_up = -1, peer_down = -1;  // communicator ranks of the row neighbours (loopback: 0, itself)
     int split = 0;               // 1: interior rows under the exchange, then the edge bands
+    int frames_launch = 0;       // vip_shard_set_frames_launch: a batch's frames in one launch
     // graph mode (vip_shard_set_graph): one captured hipGraph per (slab, out, pitch, stream)
     struct Graph {
         uint8_t* slab;
@@ -249,6 +250,24 @@ int filter_rows(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pi
     if (h->kind == VIP_FILTER_ADAPTIVE)
         return vip_adaptive_run_rows(h->ada, slab, h->pitch(), o, out_pitch, n, h->r + row0, lo, hi, s);
     return vip_bilateral_run_rows(h->bil, slab, h->pitch(), nullptr, 0, o, out_pitch, n, h->r + row0, lo, hi, s);
+}
+
+// Every own row of n frames: one launch per frame, or (vip_shard_set_frames_launch, plain
+// and adaptive filters) one launch per 4 frames (vip_*_run_rows_batch: the launch prologue
+// and tail once per launch).
+int filter_frames(const vip_shard_s* h, int n, uint8_t* const* slabs, uint8_t* const* outs, size_t out_pitch,
+                  hipStream_t s) {
+    if (h->kind == VIP_FILTER_TEXTURE || n == 1 || !h->frames_launch) {
+        for (int f = 0; f < n; ++f)
+            if (const int rc = filter_rows(h, slabs[f], outs[f], out_pitch, 0, h->own, s)) return rc;
+        return 0;
+    }
+    int lo, hi;
+    clamp_range(h, &lo, &hi);
+    const uint8_t* const* srcs = const_cast<const uint8_t* const*>(slabs);
+    if (h->kind == VIP_FILTER_ADAPTIVE)
+        return vip_adaptive_run_rows_batch(h->ada, n, srcs, h->pitch(), outs, out_pitch, h->own, h->r, lo, hi, s);
+    return vip_bilateral_run_rows_batch(h->bil, n, srcs, h->pitch(), outs, out_pitch, h->own, h->r, lo, hi, s);
 }
 
 // Interior rows [r, own - r) read only own rows; the edge bands need the halos.
@@ -503,6 +522,12 @@ int vip_shard_set_split(vip_shard_t h, int split) {
     return 0;
 }
 
+int vip_shard_set_frames_launch(vip_shard_t h, int on) {
+    if (!h || (on != 0 && on != 1)) return VIP_ERR_INVALID_ARGUMENT;
+    h->frames_launch = h->kind == VIP_FILTER_TEXTURE ? 0 : on;
+    return 0;
+}
+
 int vip_shard_set_graph(vip_shard_t h, int on) {
     if (!h || (on != 0 && on != 1)) return VIP_ERR_INVALID_ARGUMENT;
     if (h->transport != VIP_SHARD_RCCL) return VIP_ERR_INVALID_ARGUMENT;
@@ -583,11 +608,8 @@ int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* 
     DeviceGuard guard;
     const hipStream_t s = (hipStream_t)stream;
     VIP_HIP_TRY(hipSetDevice(h->device));
-    if (!h->above() && !h->below()) {  // no neighbours: the launches only
-        for (int f = 0; f < n; ++f)
-            if (const int rc = filter_rows(h, d_slabs[f], d_outs[f], out_pitch, 0, h->own, s)) return rc;
-        return 0;
-    }
+    if (!h->above() && !h->below())  // no neighbours: the launches only
+        return filter_frames(h, n, d_slabs, d_outs, out_pitch, s);
     // every frame's own rows written -> one group with all the halos on the communication stream
     VIP_HIP_TRY(hipEventRecord(h->ev_in, s));
     VIP_HIP_TRY(hipStreamWaitEvent(h->comm, h->ev_in, 0));
@@ -600,9 +622,7 @@ int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* 
     VIP_HIP_TRY(hipEventRecord(h->ev_x, h->comm));
     if (!h->split) {
         VIP_HIP_TRY(hipStreamWaitEvent(s, h->ev_x, 0));
-        for (int f = 0; f < n; ++f)
-            if ((rc = filter_rows(h, d_slabs[f], d_outs[f], out_pitch, 0, h->own, s))) return rc;
-        return 0;
+        return filter_frames(h, n, d_slabs, d_outs, out_pitch, s);
     }
     for (int f = 0; f < n; ++f)  // interiors under the exchange, then every frame's edge bands
         if ((rc = interior(h, d_slabs[f], d_outs[f], out_pitch, s))) return rc;

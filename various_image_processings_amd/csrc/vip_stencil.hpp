@@ -69,6 +69,10 @@ struct SatLut {
     static_assert(DZ >= 0 && T - B0 + (NTAB - 1) * 128 <= 65535, "ds_read immediate range");
 };
 
+// Frames one launch of the plain bilateral / adaptive kernels may filter (the
+// *_run_rows_batch entry points; a shard's B frames per RCCL group, vip_shard_run_batch).
+constexpr int kMaxBatchFrames = 4;
+
 struct StencilArgs {
     const uint8_t* src;
     const uint8_t* guide;  // == src for the plain filters
@@ -86,6 +90,14 @@ struct StencilArgs {
     int lut_nonzero;       // entries [lut_nonzero, end) of the colour LUT are exactly 0
     const float* fold;     // or null: [disc_r2_count(R)][kFoldEntries] = RN(ws(r^2) * colour[d])
     int inflight;          // host only: frames in flight on this device (the small-frame tiling's model)
+    // Multi-frame launch: frame f < nframes reads fsrc[f] and writes fdst[f] (fsrc[0] == src,
+    // fdst[0] == dst; same geometry and pitches); launch tile t is tile t - f * tiles_frame of
+    // frame f, so the persistent workgroups run straight from one frame's tiles into the
+    // next one's (one prologue, the next tile's loads under the current one's taps).
+    int nframes;
+    int tiles_frame;       // tiles per frame (set by the launcher)
+    const uint8_t* fsrc[kMaxBatchFrames];
+    uint8_t* fdst[kMaxBatchFrames];
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
 };
 
@@ -124,8 +136,15 @@ inline int device_cus() {
     return cus;
 }
 
+// VIP_PERSIST_RESERVE=k (measurement knob): persistent launches leave k CUs free, e.g. for
+// a concurrent exchange kernel
 inline int persistent_blocks(int tiles) {
-    const int cus = device_cus();
+    static const int reserve = [] {
+        const char* e = getenv("VIP_PERSIST_RESERVE");
+        return e ? atoi(e) : 0;
+    }();
+    int cus = device_cus() - reserve;
+    cus = cus > 0 ? cus : 1;
     return tiles < cus ? tiles : cus;
 }
 
@@ -673,12 +692,32 @@ __device__ __forceinline__ void finish_outputs(const f2 (&a01)[P], const f2 (&a2
     }
 }
 
-// Write P RGB outputs (3P bytes) of row oy starting at column x (A: StencilArgs or
-// RtArgs -- out_rows, width, dst, dst_pitch, dst_aligned).
+// Frame f and its tile index of launch tile mt (multi-frame launches; wave-uniform).
+struct FrameTile {
+    int f, t;
+};
+__device__ __forceinline__ FrameTile frame_tile(const StencilArgs& a, int mt) {
+    int f = 0;
+    if (a.nframes > 1)
+        while (mt >= a.tiles_frame) {
+            mt -= a.tiles_frame;
+            ++f;
+        }
+    return {f, mt};
+}
+// fsrc[f] / fdst[f] by uniform selects (no dynamic index into the kernel arguments)
+template <class T>
+__device__ __forceinline__ T frame_ptr(const T (&p)[kMaxBatchFrames], T p0, int f) {
+    static_assert(kMaxBatchFrames == 4, "frame_ptr selects");
+    return f == 0 ? p0 : f == 1 ? p[1] : f == 2 ? p[2] : p[3];
+}
+
+// Write P RGB outputs (3P bytes) of row oy starting at column x to dst (A: StencilArgs or
+// RtArgs -- out_rows, width, dst_pitch, dst_aligned).
 template <int P, class A>
-__device__ __forceinline__ void store_px(const A& a, int oy, int x, const uint32_t (&o)[P]) {
+__device__ __forceinline__ void store_px_to(const A& a, uint8_t* dst, int oy, int x, const uint32_t (&o)[P]) {
     if (oy >= a.out_rows || x >= a.width) return;
-    uint8_t* row = a.dst + (long long)oy * a.dst_pitch;
+    uint8_t* row = dst + (long long)oy * a.dst_pitch;
     if constexpr (P == 4) {
         if (a.dst_aligned && x + P <= a.width) {  // 12 bytes at a 4-byte aligned address
             uint32_t* p = reinterpret_cast<uint32_t*>(row + 3 * x);
@@ -712,6 +751,11 @@ __device__ __forceinline__ void store_px(const A& a, int oy, int x, const uint32
             }
         }
     }
+}
+
+template <int P, class A>
+__device__ __forceinline__ void store_px(const A& a, int oy, int x, const uint32_t (&o)[P]) {
+    store_px_to(a, a.dst, oy, x, o);
 }
 
 }  // namespace vip
