@@ -186,21 +186,27 @@ def halo_batches(streams: int) -> list:
 # exchange latency is about one filter launch; more streams keep the chip fed while the
 # halos of the others are in flight (and the small-slab tiling counts them, share = CUs / S).
 TRIAL_STREAMS = (2, 3, 4)
+# CUs a shared launch (one kernel for a batch's frames, vip_shard_set_frames_launch) leaves to
+# the exchange kernels and the other streams' frames. Loopback rehearsal, C2 at 8 GPUs, 3
+# frames per group: 0 free 0.0335, 16 free 0.0268 ms per step, against 0.0311 one launch per
+# frame (profiles/r04_shared_launch.txt).
+SHARED_FREE_CUS = (0, 16, 32)
 
 
 def native_forms(stream_counts, texture: bool, graph: bool) -> list:
     """The N > 1 native trial's forms (S streams, split, B frames per RCCL group, graph,
-    shared launches): every S with each B that keeps a buffer on one stream (halo_batches),
-    the split / one-launch pair (the texture filter has no split), with `graph` one captured
-    form per (S, split), and for B > 1 after the exchange the B frames in shared launches
-    (vip_shard_set_frames_launch; plain and adaptive filters)."""
+    shared): every S with each B that keeps a buffer on one stream (halo_batches), the split /
+    one-launch pair (the texture filter has no split), with `graph` one captured form per
+    (S, split), and for B > 1 after the exchange the B frames in shared launches
+    (vip_shard_set_frames_launch; plain and adaptive filters) leaving each of SHARED_FREE_CUS
+    CUs free. shared is None for one launch per frame, else that free-CU count."""
     forms = []
     for n in stream_counts:
         for split in ((False,) if texture else (True, False)):
-            forms += [(n, split, b, False, False) for b in halo_batches(n)]
-            forms += [(n, split, 1, True, False)] if graph else []
+            forms += [(n, split, b, False, None) for b in halo_batches(n)]
+            forms += [(n, split, 1, True, None)] if graph else []
             if not split and not texture:
-                forms += [(n, split, b, False, True) for b in halo_batches(n) if b > 1]
+                forms += [(n, split, b, False, fc) for b in halo_batches(n) if b > 1 for fc in SHARED_FREE_CUS]
     return forms
 BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
 
@@ -832,7 +838,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             for x in shards:
                 x.set_split(split)
                 x.set_graph(graph)
-                x.set_frames_launch(shared)
+                x.set_frames_launch(shared is not None, shared or 0)
             hb["B"], hb["S"] = b, n_s
             for _ in range(NBUF):  # untimed: captures every (buffer, stream) graph in graph mode
                 step(i_settle)
@@ -855,15 +861,15 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         for x in shards:
             x.set_split(best_split)
             x.set_graph(best_graph)
-            x.set_frames_launch(best_shared)
+            x.set_frames_launch(best_shared is not None, best_shared or 0)
         hb["B"], hb["S"] = best_b, best_s
         res["streams"] = best_s
         res["exchange"] += ("; interior rows overlapped with the exchange, then the edge bands" if best_split
                             else "; one launch over the own rows after the exchange")
         if best_b > 1:
             res["exchange"] += f"; the halos of {best_b} frames per RCCL group"
-            if best_shared:
-                res["exchange"] += ", filtered in one launch"
+            if best_shared is not None:
+                res["exchange"] += ", filtered in one launch" + (f" leaving {best_shared} CUs free" if best_shared else "")
         if best_graph:
             res["exchange"] += "; each frame replayed from a captured hipGraph"
         res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best_split
@@ -871,7 +877,9 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
                             graph=best_graph, frames_launch=best_shared,
                             trial_ms_per_step={(f"s{s_}_" if len(s_forms) > 1 else "")
                                                + ("split" if sp_ else "one_launch") + (f"_batch{b_}" if b_ > 1 else "")
-                                               + ("_graph" if g_ else "") + ("_one_kernel" if sh_ else ""): round(v, 4)
+                                               + ("_graph" if g_ else "")
+                                               + ("" if sh_ is None else "_one_kernel" + (f"_free{sh_}" if sh_ else "")):
+                                               round(v, 4)
                                                for (s_, sp_, b_, g_, sh_), v in trial.items()})
         res["halo_batch"] = best_b
     res["settle_steps"] = i_settle

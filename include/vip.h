@@ -132,11 +132,13 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
  * vip_bilateral_run_rows(h, d_srcs[f], src_pitch, NULL, 0, d_dsts[f], dst_pitch, out_rows,
  * src_row0, row_lo, row_hi, stream) would, with up to 4 frames per launch: the persistent
  * workgroups run from one frame's tiles into the next one's, so a small slab's launch
- * prologue and tail are paid once per launch. VIP_ERR_ALIASING when any d_dsts[f] equals
- * any d_srcs[g]. Results are identical to the per-frame calls. */
+ * prologue and tail are paid once per launch. free_cus >= 0: CUs the launch leaves to
+ * concurrent work (another stream's frames, an exchange kernel); 0 = all CUs.
+ * VIP_ERR_ALIASING when any d_dsts[f] equals any d_srcs[g]. Results are identical to the
+ * per-frame calls. */
 int vip_bilateral_run_rows_batch(vip_bilateral_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
                                  uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
-                                 int row_hi, void* stream);
+                                 int row_hi, int free_cus, void* stream);
 /* Tuning knob, process-wide (no reference counterpart): waves per workgroup of the plain
  * bilateral kernel for radius <= 8. 0 (default) = chosen per launch from the frame's
  * tile count (small frames take 8 or 4 waves and smaller tiles so more CUs work);
@@ -170,7 +172,7 @@ int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pit
 /* n frames per launch (up to 4), as vip_bilateral_run_rows_batch */
 int vip_adaptive_run_rows_batch(vip_adaptive_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
                                 uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
-                                int row_hi, void* stream);
+                                int row_hi, int free_cus, void* stream);
 
 /* ---- gradient magnitude: cuda_gradient<T> (include/cuda/gradient.hpp:4-23, src/gradient_impl.cu:90-112) ---- */
 int vip_gradient_u8(const uint8_t* d_src, float* d_dst, int width, int height, int src_ch, int numerics,

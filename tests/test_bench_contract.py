@@ -233,9 +233,9 @@ def test_native_trial_forms_keep_buffers_on_one_stream():
     assert all(bench.NBUF % (s * b) == 0 and not g for s, _, b, g, _ in forms)
     assert {(s, sp) for s, sp, _, _, _ in forms} == {(s, sp) for s in bench.TRIAL_STREAMS for sp in (True, False)}
     # shared launches: only after the exchange (no split) and for more than one frame
-    assert all(not sp and b > 1 for _, sp, b, _, sh in forms if sh)
-    assert {(s, b) for s, _, b, _, sh in forms if sh} == {(s, b) for s in bench.TRIAL_STREAMS
-                                                         for b in bench.halo_batches(s) if b > 1}
+    assert all(not sp and b > 1 for _, sp, b, _, sh in forms if sh is not None)
+    assert {(s, b, sh) for s, _, b, _, sh in forms if sh is not None} == {
+        (s, b, fc) for s in bench.TRIAL_STREAMS for b in bench.halo_batches(s) if b > 1 for fc in bench.SHARED_FREE_CUS}
     tex = bench.native_forms([2], texture=True, graph=True)
-    assert all(not sp and not sh for _, sp, _, _, sh in tex) and [f for f in tex if f[3]] == [(2, False, 1, True, False)]
+    assert all(not sp and sh is None for _, sp, _, _, sh in tex) and [f for f in tex if f[3]] == [(2, False, 1, True, None)]
     assert len(set(forms)) == len(forms)

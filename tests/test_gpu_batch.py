@@ -34,17 +34,19 @@ def test_batch_equals_oracle_per_frame(dev, oracle, kind, k, n):
 
 
 @pytest.mark.parametrize("kind", ["bilateral", "adaptive"])
-def test_batch_small_slab_tiling(dev, oracle, kind):
+@pytest.mark.parametrize("free_cus", [0, 16, 250, 10000])
+def test_batch_small_slab_tiling(dev, oracle, kind, free_cus):
     """C2's slab at 8 GPUs (3840 x 270 own rows + two 7-row halos), 3 frames in one launch:
-    the small-slab tiling is planned for all three frames' tiles. Every frame equals its
-    own run_rows launch; frame 0 equals the oracle."""
+    the small-slab tiling is planned for all three frames' tiles, and the persistent
+    workgroups leave free_cus CUs free (at least one workgroup runs: 10000 leaves one).
+    Every frame equals its own run_rows launch; frame 0 equals the oracle."""
     w, r, own = 3840, 7, 270
     rows = own + 2 * r
     imgs = _slabs(oracle, 3, w, rows)
     impl = (_BilateralImpl if kind == "bilateral" else _AdaptiveImpl)(w, rows, 2 * r + 1)
     srcs = [dev.put(x) for x in imgs]
     dsts = [dev.empty((own, w, 3)) for _ in range(3)]
-    impl.run_rows_batch(srcs, dsts, own, r, 0, rows)
+    impl.run_rows_batch(srcs, dsts, own, r, 0, rows, free_cus=free_cus)
     for f in range(3):
         one = dev.empty((own, w, 3))
         impl.run_rows(srcs[f], one, own, r, 0, rows)

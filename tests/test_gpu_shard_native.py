@@ -313,18 +313,19 @@ def test_loopback_timed_events_in_order(dev, oracle):
                 assert t1 <= t2 + 1e-3
 
 
-@pytest.mark.parametrize("split,shared", [(False, False), (True, False), (False, True)])
+@pytest.mark.parametrize("split,shared", [(False, None), (True, None), (False, 0), (False, 16)])
 @pytest.mark.parametrize("adaptive", [False, True])
 def test_loopback_batch(dev, oracle, split, shared, adaptive):
     """vip_shard_run_batch with neighbours: the halos of three frames in one RCCL group;
-    shared: the three frames filtered in one launch (vip_shard_set_frames_launch)."""
+    shared (not None): the three frames filtered in one launch leaving that many CUs free
+    (vip_shard_set_frames_launch)."""
     torch = dev.torch_
     w, own = 900, 200
     imgs = [oracle.random_image(w, own), np.ascontiguousarray(oracle.random_image(w, own)[::-1])]
     imgs.append(np.ascontiguousarray(imgs[0][:, ::-1]))
     s = NativeShard(w, 4 * own, 15, 2, 4, None, adaptive=adaptive, loopback=True)
     s.set_split(split)
-    s.set_frames_launch(shared)
+    s.set_frames_launch(shared is not None, shared or 0)
     slabs = [_loopback_slab(dev, s, im) for im in imgs]
     outs = [dev.empty((own, w, 3)) for _ in imgs]
     s.batch_launcher()([t.data_ptr() for t in slabs], [t.data_ptr() for t in outs],

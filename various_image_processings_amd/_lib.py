@@ -66,7 +66,7 @@ SIGNATURES = {
                  _c_int, _c_int, _c_int, _c_int, _c_void_p]),
     "vip_bilateral_run_rows_batch": (
         _c_int, [_c_void_p, _c_int, ctypes.POINTER(_c_void_p), _c_size_t, ctypes.POINTER(_c_void_p), _c_size_t,
-                 _c_int, _c_int, _c_int, _c_int, _c_void_p]),
+                 _c_int, _c_int, _c_int, _c_int, _c_int, _c_void_p]),
     "vip_adaptive_create": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_int, _c_float, _c_float, _c_int]),
     "vip_adaptive_destroy": (_c_int, [_c_void_p]),
     "vip_adaptive_run": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p, _c_size_t, _c_void_p]),
@@ -74,7 +74,7 @@ SIGNATURES = {
         _c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p, _c_size_t, _c_int, _c_int, _c_int, _c_int, _c_void_p]),
     "vip_adaptive_run_rows_batch": (
         _c_int, [_c_void_p, _c_int, ctypes.POINTER(_c_void_p), _c_size_t, ctypes.POINTER(_c_void_p), _c_size_t,
-                 _c_int, _c_int, _c_int, _c_int, _c_void_p]),
+                 _c_int, _c_int, _c_int, _c_int, _c_int, _c_void_p]),
     "vip_gradient_u8": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p]),
     "vip_gradient_f32": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p]),
     "vip_texture_create": (_c_int, [ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_int, _c_int, _c_int]),

@@ -36,7 +36,7 @@ SIGNATURES = {
     "vip_shard_run_batch": (_i, [_p, _i, _pp, _pp, _s, _p]),
     "vip_shard_run_group": (_i, [_pp, _i, _pp, _pp, _s, _pp]),
     "vip_shard_set_graph": (_i, [_p, _i]),
-    "vip_shard_set_frames_launch": (_i, [_p, _i]),
+    "vip_shard_set_frames_launch": (_i, [_p, _i, _i]),
     "vip_shard_graph_count": (_i, [_p, _ip]),
     "vip_shard_create_loopback": (_i, [_pp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _i, _i]),
     "vip_shard_last_error": (ctypes.c_char_p, []),

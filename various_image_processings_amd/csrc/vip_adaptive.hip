@@ -330,7 +330,7 @@ static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     args.tiles_frame = args.tiles_x * ((a.out_rows + TH - 1) / TH);
     args.tiles_total = args.tiles_frame * (a.nframes < 1 ? 1 : a.nframes);
     if (args.tiles_total == 0) return 0;
-    const int blocks = persistent_blocks(args.tiles_total);
+    const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }

@@ -283,7 +283,7 @@ struct Tiling {
 inline Tiling small_frame_tiling(int width, int out_rows, int inflight = 1, int nframes = 1) {
     const int forced = bilateral_forced_waves();
     const int fwide = bilateral_forced_wide();  // 0 auto, 1 narrow, 2 wide
-    const int share = device_cus() / (inflight > 1 ? inflight : 1);  // CUs per frame
+    const int share = device_cus() / (inflight > 1 ? inflight : 1);  // CUs per launch
     const int cus = share > 0 ? share : 1;
     const int cand[3] = {16, 8, 4};
     const float cost[3] = {1.0f, 1.25f, 1.8f};
@@ -377,7 +377,7 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     args.tiles_frame = args.tiles_x * ((a.out_rows + TH - 1) / TH);
     args.tiles_total = args.tiles_frame * (JOINT || a.nframes < 1 ? 1 : a.nframes);  // the joint filter: one frame
     if (args.tiles_total == 0) return 0;
-    const int blocks = persistent_blocks(args.tiles_total);
+    const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }

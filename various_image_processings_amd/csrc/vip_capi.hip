@@ -160,6 +160,7 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.inflight = 1;
     a.nframes = 1;
     a.tiles_frame = 0;
+    a.free_cus = 0;
     for (int f = 0; f < kMaxBatchFrames; ++f) {
         a.fsrc[f] = src;
         a.fdst[f] = dst;
@@ -516,8 +517,9 @@ static int check_batch(int n, const uint8_t* const* srcs, uint8_t* const* dsts) 
 
 int vip_bilateral_run_rows_batch(vip_bilateral_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
                                  uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
-                                 int row_hi, void* stream) {
-    if (!h || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+                                 int row_hi, int free_cus, void* stream) {
+    if (!h || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi || free_cus < 0)
+        return VIP_ERR_INVALID_ARGUMENT;
     if (const int rc = check_batch(n, d_srcs, d_dsts)) return rc;
     const hipStream_t s = (hipStream_t)stream;
     if (use_runtime_kernel(h->radius)) {  // the runtime-radius kernel: one launch per frame
@@ -534,6 +536,7 @@ int vip_bilateral_run_rows_batch(vip_bilateral_t h, int n, const uint8_t* const*
                   src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, nullptr, h->wsq);
         fill_batch(a, m, d_srcs + f0, src_pitch, d_dsts + f0, dst_pitch);
         a.inflight = frames_in_flight(s);
+        a.free_cus = free_cus;
         if (const int rc = launch_bilateral(h->radius, false, h->numerics == VIP_NUMERICS_CUDA, a, s)) return rc;
     }
     return 0;
@@ -603,8 +606,9 @@ int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pit
 
 int vip_adaptive_run_rows_batch(vip_adaptive_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
                                 uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
-                                int row_hi, void* stream) {
-    if (!h || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi) return VIP_ERR_INVALID_ARGUMENT;
+                                int row_hi, int free_cus, void* stream) {
+    if (!h || out_rows < 0 || row_lo < 0 || row_hi > h->height || row_lo >= row_hi || free_cus < 0)
+        return VIP_ERR_INVALID_ARGUMENT;
     if (const int rc = check_batch(n, d_srcs, d_dsts)) return rc;
     const hipStream_t s = (hipStream_t)stream;
     if (use_runtime_kernel(h->radius)) {
@@ -620,6 +624,7 @@ int vip_adaptive_run_rows_batch(vip_adaptive_t h, int n, const uint8_t* const* d
         fill_args(a, h->width, d_srcs[f0], src_pitch, d_srcs[f0], src_pitch, d_dsts[f0], dst_pitch, out_rows,
                   src_row0, row_lo, row_hi, h->d_color, h->lut_nonzero, nullptr, h->wsq);
         fill_batch(a, m, d_srcs + f0, src_pitch, d_dsts + f0, dst_pitch);
+        a.free_cus = free_cus;
         if (const int rc = launch_adaptive(h->radius, h->numerics == VIP_NUMERICS_CUDA, a, s)) return rc;
     }
     return 0;

@@ -115,6 +115,7 @@ struct vip_shard_s {
     int peer_up = -1, peer_down = -1;  // communicator ranks of the row neighbours (loopback: 0, itself)
     int split = 0;               // 1: interior rows under the exchange, then the edge bands
     int frames_launch = 0;       // vip_shard_set_frames_launch: a batch's frames in one launch
+    int free_cus = 0;            // ... leaving this many CUs to concurrent work
     // graph mode (vip_shard_set_graph): one captured hipGraph per (slab, out, pitch, stream)
     struct Graph {
         uint8_t* slab;
@@ -266,8 +267,10 @@ int filter_frames(const vip_shard_s* h, int n, uint8_t* const* slabs, uint8_t* c
     clamp_range(h, &lo, &hi);
     const uint8_t* const* srcs = const_cast<const uint8_t* const*>(slabs);
     if (h->kind == VIP_FILTER_ADAPTIVE)
-        return vip_adaptive_run_rows_batch(h->ada, n, srcs, h->pitch(), outs, out_pitch, h->own, h->r, lo, hi, s);
-    return vip_bilateral_run_rows_batch(h->bil, n, srcs, h->pitch(), outs, out_pitch, h->own, h->r, lo, hi, s);
+        return vip_adaptive_run_rows_batch(h->ada, n, srcs, h->pitch(), outs, out_pitch, h->own, h->r, lo, hi,
+                                           h->free_cus, s);
+    return vip_bilateral_run_rows_batch(h->bil, n, srcs, h->pitch(), outs, out_pitch, h->own, h->r, lo, hi,
+                                        h->free_cus, s);
 }
 
 // Interior rows [r, own - r) read only own rows; the edge bands need the halos.
@@ -522,9 +525,10 @@ int vip_shard_set_split(vip_shard_t h, int split) {
     return 0;
 }
 
-int vip_shard_set_frames_launch(vip_shard_t h, int on) {
-    if (!h || (on != 0 && on != 1)) return VIP_ERR_INVALID_ARGUMENT;
+int vip_shard_set_frames_launch(vip_shard_t h, int on, int free_cus) {
+    if (!h || (on != 0 && on != 1) || free_cus < 0) return VIP_ERR_INVALID_ARGUMENT;
     h->frames_launch = h->kind == VIP_FILTER_TEXTURE ? 0 : on;
+    h->free_cus = free_cus;
     return 0;
 }
 

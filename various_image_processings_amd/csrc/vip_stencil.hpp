@@ -96,6 +96,7 @@ struct StencilArgs {
     // next one's (one prologue, the next tile's loads under the current one's taps).
     int nframes;
     int tiles_frame;       // tiles per frame (set by the launcher)
+    int free_cus;          // host only: persistent workgroups leave this many CUs to concurrent work
     const uint8_t* fsrc[kMaxBatchFrames];
     uint8_t* fdst[kMaxBatchFrames];
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
@@ -136,14 +137,9 @@ inline int device_cus() {
     return cus;
 }
 
-// VIP_PERSIST_RESERVE=k (measurement knob): persistent launches leave k CUs free, e.g. for
-// a concurrent exchange kernel
-inline int persistent_blocks(int tiles) {
-    static const int reserve = [] {
-        const char* e = getenv("VIP_PERSIST_RESERVE");
-        return e ? atoi(e) : 0;
-    }();
-    int cus = device_cus() - reserve;
+// free_cus: CUs the launch leaves to concurrent work (StencilArgs::free_cus)
+inline int persistent_blocks(int tiles, int free_cus = 0) {
+    int cus = device_cus() - (free_cus > 0 ? free_cus : 0);
     cus = cus > 0 ? cus : 1;
     return tiles < cus ? tiles : cus;
 }

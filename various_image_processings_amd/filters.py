@@ -168,20 +168,21 @@ class _BilateralImpl(_Handle):
         call("vip_bilateral_run_rows", self._h, _ptr(d_src, p * int(row_hi)), p, g, p, _ptr(d_dst, p * int(out_rows)),
              p, int(out_rows), int(src_row0), int(row_lo), int(row_hi), _stream(stream))
 
-    def run_rows_batch(self, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, stream=None):
+    def run_rows_batch(self, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, free_cus=0, stream=None):
         """run_rows over several frames of the same geometry, up to 4 per launch
         (include/vip.h vip_bilateral_run_rows_batch)."""
         _run_batch("vip_bilateral_run_rows_batch", self._h, self.width * 3, d_srcs, d_dsts, out_rows, src_row0,
-                   row_lo, row_hi, stream)
+                   row_lo, row_hi, free_cus, stream)
 
 
-def _run_batch(name, h, p, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, stream):
+def _run_batch(name, h, p, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, free_cus, stream):
     if len(d_srcs) != len(d_dsts):
         raise ValueError("one output per input frame")
     n = len(d_srcs)
     srcs = (ctypes.c_void_p * max(n, 1))(*[_ptr(x, p * int(row_hi)) for x in d_srcs])
     dsts = (ctypes.c_void_p * max(n, 1))(*[_ptr(x, p * int(out_rows)) for x in d_dsts])
-    call(name, h, n, srcs, p, dsts, p, int(out_rows), int(src_row0), int(row_lo), int(row_hi), _stream(stream))
+    call(name, h, n, srcs, p, dsts, p, int(out_rows), int(src_row0), int(row_lo), int(row_hi), int(free_cus),
+         _stream(stream))
 
 
 class CudaBilateralFilter:
@@ -218,10 +219,10 @@ class _AdaptiveImpl(_Handle):
         call("vip_adaptive_run_rows", self._h, _ptr(d_src, p * int(row_hi)), p, _ptr(d_dst, p * int(out_rows)), p,
              int(out_rows), int(src_row0), int(row_lo), int(row_hi), _stream(stream))
 
-    def run_rows_batch(self, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, stream=None):
+    def run_rows_batch(self, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, free_cus=0, stream=None):
         """include/vip.h vip_adaptive_run_rows_batch"""
         _run_batch("vip_adaptive_run_rows_batch", self._h, self.width * 3, d_srcs, d_dsts, out_rows, src_row0,
-                   row_lo, row_hi, stream)
+                   row_lo, row_hi, free_cus, stream)
 
 
 class CudaAdaptiveBilateralFilter:

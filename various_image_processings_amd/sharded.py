@@ -351,11 +351,11 @@ class NativeShard:
         from . import _shard_lib as S
         S.call("vip_shard_set_graph", self._h, 1 if on else 0)
 
-    def set_frames_launch(self, on: bool) -> None:
-        """vip_shard_set_frames_launch: a batch's frames share filter launches (True) or
-        launch one by one (False, the default)."""
+    def set_frames_launch(self, on: bool, free_cus: int = 0) -> None:
+        """vip_shard_set_frames_launch: a batch's frames share filter launches that leave
+        free_cus CUs to concurrent work (True) or launch one by one (False, the default)."""
         from . import _shard_lib as S
-        S.call("vip_shard_set_frames_launch", self._h, 1 if on else 0)
+        S.call("vip_shard_set_frames_launch", self._h, 1 if on else 0, int(free_cus))
 
     def graph_count(self) -> int:
         import ctypes
