@@ -190,7 +190,7 @@ TRIAL_STREAMS = (2, 3, 4)
 # the exchange kernels and the other streams' frames. Loopback rehearsal, C2 at 8 GPUs, 3
 # frames per group: 0 free 0.0335, 16 free 0.0268 ms per step, against 0.0311 one launch per
 # frame (profiles/r04_shared_launch.txt).
-SHARED_FREE_CUS = (0, 16, 32)
+SHARED_FREE_CUS = (0, 8, 16, 24, 32)
 
 
 def native_forms(stream_counts, texture: bool, graph: bool) -> list:

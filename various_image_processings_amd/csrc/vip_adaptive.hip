@@ -291,7 +291,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
 
             uint32_t o[P];
             finish_outputs(a01, a2k, o);
-            store_px_to(a, frame_ptr(a.fdst, a.dst, ft.f), ty0 + ty, tx0 + tx * P, o);
+            store_px_to(a, frame_dst(a, tile), ty0 + ty, tx0 + tx * P, o);
         }
         if (next >= a.tiles_total) break;
         __syncthreads();

@@ -184,7 +184,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
 
             uint32_t o[P];
             finish_outputs<P, VIP_BIL_RCP != 0>(a01, a2k, o);
-            store_px_to(a, JOINT ? a.dst : frame_ptr(a.fdst, a.dst, ft.f), ty0 + ty, tx0 + tx * P, o);
+            store_px_to(a, JOINT ? a.dst : frame_dst(a, tile), ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);
         if (next >= a.tiles_total) {

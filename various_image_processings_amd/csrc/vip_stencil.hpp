@@ -694,18 +694,36 @@ struct FrameTile {
 };
 __device__ __forceinline__ FrameTile frame_tile(const StencilArgs& a, int mt) {
     int f = 0;
-    if (a.nframes > 1)
-        while (mt >= a.tiles_frame) {
-            mt -= a.tiles_frame;
-            ++f;
-        }
+#ifdef VIP_NO_MULTIFRAME  // measurement builds only: single-frame kernels (batch launches filter frame 0 only)
+    return {f, mt};
+#endif
+    // a one-frame launch has tiles_frame == tiles_total > mt; never loops on tiles_frame <= 0
+    while (mt >= a.tiles_frame && a.tiles_frame > 0 && f < kMaxBatchFrames - 1) {
+        mt -= a.tiles_frame;
+        ++f;
+    }
     return {f, mt};
 }
+// Output base of launch tile `tile`'s frame, derived again at the store: keeping the frame
+// index live across the tap loop costs scalar registers the loop's spatial weights use
+// (measured +1 % on the 4K r=7 launch).
+__device__ __forceinline__ uint8_t* frame_dst(const StencilArgs& a, int tile) {
+    __asm__ volatile("" : "+s"(tile));  // recompute here, not from the tile's start
+    int mt = xcd_tile(tile, a.tiles_total), f = 0;
+    while (mt >= a.tiles_frame && a.tiles_frame > 0 && f < kMaxBatchFrames - 1) {
+        mt -= a.tiles_frame;
+        ++f;
+    }
+    return a.fdst[f];  // one scalar load at the store (kernel arguments), nothing held across the taps
+}
+
 // fsrc[f] / fdst[f] by uniform selects (no dynamic index into the kernel arguments)
 template <class T>
 __device__ __forceinline__ T frame_ptr(const T (&p)[kMaxBatchFrames], T p0, int f) {
-    static_assert(kMaxBatchFrames == 4, "frame_ptr selects");
-    return f == 0 ? p0 : f == 1 ? p[1] : f == 2 ? p[2] : p[3];
+#ifdef VIP_NO_MULTIFRAME
+    return p0;
+#endif
+    return f == 0 ? p0 : p[f];  // a scalar load when needed, not four pointers held in SGPRs
 }
 
 // Write P RGB outputs (3P bytes) of row oy starting at column x to dst (A: StencilArgs or
