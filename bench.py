@@ -208,6 +208,8 @@ def native_forms(stream_counts, texture: bool, graph: bool) -> list:
             if not split and not texture:
                 forms += [(n, split, b, False, fc) for b in halo_batches(n) if b > 1 for fc in SHARED_FREE_CUS]
     return forms
+
+
 BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
 
 
