@@ -178,7 +178,7 @@ def halo_batches(streams: int) -> list:
     runs in batch i // B on stream (i // B) % S, so B * S must divide NBUF for buffer
     i % NBUF to always meet the same stream (its halo receive then stays ordered after its
     last reader)."""
-    return [b for b in (1, 2, 3) if NBUF % (b * streams) == 0]
+    return [b for b in (1, 2, 3, 4, 6) if NBUF % (b * streams) == 0]
 
 
 # N > 1 native: frames in flight the trial may use when neither --streams nor the config
@@ -835,7 +835,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # With several stream counts (TRIAL_STREAMS), S is a trial dimension too: frames in
         # flight hide one stream's exchange latency behind the others' launches.
         trial = {}
-        n_trial = 42  # a multiple of every B
+        n_trial = 48  # a multiple of every B
         for n_s, split, b, graph, shared in native_forms(s_forms, cfg["kind"] == "texture", bool(args.graph)):
             for x in shards:
                 x.set_split(split)

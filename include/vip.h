@@ -130,7 +130,7 @@ int vip_bilateral_run_rows(vip_bilateral_t h, const uint8_t* d_src, size_t src_p
 /* n frames of the same geometry (no reference counterpart; a shard's frames per RCCL group,
  * vip_shard_run_batch): frame f filters d_srcs[f] into d_dsts[f] exactly as
  * vip_bilateral_run_rows(h, d_srcs[f], src_pitch, NULL, 0, d_dsts[f], dst_pitch, out_rows,
- * src_row0, row_lo, row_hi, stream) would, with up to 4 frames per launch: the persistent
+ * src_row0, row_lo, row_hi, stream) would, with up to 6 frames per launch: the persistent
  * workgroups run from one frame's tiles into the next one's, so a small slab's launch
  * prologue and tail are paid once per launch. free_cus >= 0: CUs the launch leaves to
  * concurrent work (another stream's frames, an exchange kernel); 0 = all CUs.
@@ -169,7 +169,7 @@ int vip_adaptive_run(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, u
                      void* stream);
 int vip_adaptive_run_rows(vip_adaptive_t h, const uint8_t* d_src, size_t src_pitch, uint8_t* d_dst, size_t dst_pitch,
                           int out_rows, int src_row0, int row_lo, int row_hi, void* stream);
-/* n frames per launch (up to 4), as vip_bilateral_run_rows_batch */
+/* n frames per launch (up to 6), as vip_bilateral_run_rows_batch */
 int vip_adaptive_run_rows_batch(vip_adaptive_t h, int n, const uint8_t* const* d_srcs, size_t src_pitch,
                                 uint8_t* const* d_dsts, size_t dst_pitch, int out_rows, int src_row0, int row_lo,
                                 int row_hi, int free_cus, void* stream);

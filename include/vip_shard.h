@@ -133,7 +133,7 @@ int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* 
                         void* stream);
 
 /* 0 (default): vip_shard_run_batch launches the filter once per frame; 1: the frames of a
- * batch (split 0, plain or adaptive filter) share launches, up to 4 per launch
+ * batch (split 0, plain or adaptive filter) share launches, up to 6 per launch
  * (vip_bilateral_run_rows_batch / vip_adaptive_run_rows_batch), which leave free_cus CUs to
  * the exchange kernels and the other streams' frames. Same bytes either way; which is
  * faster depends on how the launches meet the exchange kernels (measured per run by

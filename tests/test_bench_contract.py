@@ -127,7 +127,7 @@ def test_halo_batches_keep_buffers_on_one_stream():
             for i in range(10 * bench.NBUF * B):
                 st = (i // B) % S
                 assert seen.setdefault(i % bench.NBUF, st) == st
-    assert bench.halo_batches(2) == [1, 2, 3]
+    assert bench.halo_batches(2) == [1, 2, 3, 6] and bench.halo_batches(3) == [1, 2, 4]
 
 
 # --- `python bench.py --gpus N` starts its own N ranks -------------

@@ -1,5 +1,5 @@
 """Multi-frame launches (include/vip.h vip_bilateral_run_rows_batch / vip_adaptive_run_rows_batch):
-n frames of one geometry, up to 4 per launch, each frame bit-exact with its own run_rows call
+n frames of one geometry, up to 6 per launch, each frame bit-exact with its own run_rows call
 and with the oracle. These launches carry a shard's B frames per RCCL group
 (vip_shard_run_batch; tests/test_gpu_shard_native.py covers that path end to end)."""
 import numpy as np
@@ -17,11 +17,11 @@ def _slabs(oracle, n, w, rows):
 
 @pytest.mark.parametrize("kind,k", [("bilateral", 3), ("bilateral", 15), ("bilateral", 31), ("adaptive", 9),
                                     ("adaptive", 15)])
-@pytest.mark.parametrize("n", [1, 2, 3, 5])
+@pytest.mark.parametrize("n", [1, 2, 3, 6, 7])
 def test_batch_equals_oracle_per_frame(dev, oracle, kind, k, n):
     """A 54-row slab per frame, 40 output rows centred 7 rows down, neighbours clamped to
-    the slab: frame f's output is rows 7..46 of the oracle's filter of that slab. n = 5 is
-    two launches (4 + 1)."""
+    the slab: frame f's output is rows 7..46 of the oracle's filter of that slab. n = 7 is
+    two launches (6 + 1)."""
     w, rows, out_rows, row0 = 200, 54, 40, 7
     imgs = _slabs(oracle, n, w, rows)
     impl = (_BilateralImpl if kind == "bilateral" else _AdaptiveImpl)(w, rows, k)

@@ -254,7 +254,7 @@ int filter_rows(const vip_shard_s* h, uint8_t* slab, uint8_t* out, size_t out_pi
 }
 
 // Every own row of n frames: one launch per frame, or (vip_shard_set_frames_launch, plain
-// and adaptive filters) one launch per 4 frames (vip_*_run_rows_batch: the launch prologue
+// and adaptive filters) one launch per 6 frames (vip_*_run_rows_batch: the launch prologue
 // and tail once per launch).
 int filter_frames(const vip_shard_s* h, int n, uint8_t* const* slabs, uint8_t* const* outs, size_t out_pitch,
                   hipStream_t s) {

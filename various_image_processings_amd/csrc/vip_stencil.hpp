@@ -71,7 +71,7 @@ struct SatLut {
 
 // Frames one launch of the plain bilateral / adaptive kernels may filter (the
 // *_run_rows_batch entry points; a shard's B frames per RCCL group, vip_shard_run_batch).
-constexpr int kMaxBatchFrames = 4;
+constexpr int kMaxBatchFrames = 6;
 
 struct StencilArgs {
     const uint8_t* src;

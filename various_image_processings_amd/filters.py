@@ -169,7 +169,7 @@ class _BilateralImpl(_Handle):
              p, int(out_rows), int(src_row0), int(row_lo), int(row_hi), _stream(stream))
 
     def run_rows_batch(self, d_srcs, d_dsts, out_rows, src_row0, row_lo, row_hi, free_cus=0, stream=None):
-        """run_rows over several frames of the same geometry, up to 4 per launch
+        """run_rows over several frames of the same geometry, up to 6 per launch
         (include/vip.h vip_bilateral_run_rows_batch)."""
         _run_batch("vip_bilateral_run_rows_batch", self._h, self.width * 3, d_srcs, d_dsts, out_rows, src_row0,
                    row_lo, row_hi, free_cus, stream)
