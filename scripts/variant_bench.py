@@ -10,6 +10,9 @@ import sys, json, torch, ctypes
 sys.path.insert(0, ".")
 import various_image_processings_amd._lib as L
 L.LIB_PATH = sys.argv[1]
+_h = ctypes.CDLL(sys.argv[1])  # an older build lacks newer entry points: bind only what it has
+for _n in [n for n in L.SIGNATURES if not hasattr(_h, n)]:
+    del L.SIGNATURES[_n]
 from various_image_processings_amd.filters import _BilateralImpl, _AdaptiveImpl, _TextureImpl
 torch.cuda.set_device(0)
 W, H = 3840, 2160
