@@ -433,8 +433,10 @@ def pmc_traffic(config: str, kernels: list, per_step: int = 1):
 
 
 def launched(kernels: list, prefix: str):
-    """The launched kernel (exact name) that starts with prefix, or None."""
-    hit = [k for k in kernels if k.startswith(prefix)]
+    """The launched kernel (exact name) that starts with prefix, or None; a shared launch's
+    multi-frame form of it (`..._frames_kernel<`, vip_*_run_rows_batch) counts too."""
+    frames = prefix.replace("_kernel<", "_frames_kernel<")
+    hit = [k for k in kernels if k.startswith(prefix)] + [k for k in kernels if k.startswith(frames)]
     return hit[0] if hit else None
 
 

@@ -43,8 +43,9 @@ constexpr int kAdaSatT = 16;                         // round_up(kAdaSatB0, 16):
 template <int NE, bool SAT>
 constexpr int ada_lut_words() { return NE * (NE < 1536 ? 32 : 16) + (SAT ? kAdaSatT / 4 : 0); }
 
-template <int R, int WAVES, bool FMA, int P, int NE = 1536, bool SAT = false>
-__global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs a) {
+// The kernel body; MULTI: a multi-frame launch (adaptive_frames_kernel, as bilateral_body)
+template <int R, int WAVES, bool FMA, int P, int NE, bool SAT, bool MULTI>
+__device__ __forceinline__ void adaptive_body(const StencilArgs& a) {
     static_assert(!SAT || NE == 512, "SAT: 512 entries x 32 copies");
     using G = Geom<R, P>;
     constexpr int NT = WAVES * 64;
@@ -88,20 +89,20 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
     LutStage<NT, NE, COPIES> ls;  // LUT reads go out before the first tile's
     ls.load(a.color);
     {  // multi-frame launches: frame f's tiles follow frame f - 1's
-        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
-        pf.issue(frame_ptr(a.fsrc, a.src, ft.f), a.src_pitch, a, (ft.t % a.tiles_x) * G::TW, (ft.t / a.tiles_x) * TH);
+        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
+        pf.issue(frame_src<MULTI>(a.src, ft.f), a.src_pitch, a, (ft.t % a.tiles_x) * G::TW, (ft.t / a.tiles_x) * TH);
     }
     ls.store(lut);
     pf.commit(plane);
     __syncthreads();
 
     while (true) {
-        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
         const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
         if (next < a.tiles_total) {
-            const FrameTile fn = frame_tile(a, xcd_tile(next, a.tiles_total));
-            pf.issue(frame_ptr(a.fsrc, a.src, fn.f), a.src_pitch, a, (fn.t % a.tiles_x) * G::TW,
+            const FrameTile fn = frame_tile<MULTI>(a, xcd_tile(next, a.tiles_total));
+            pf.issue(frame_src<MULTI>(a.src, fn.f), a.src_pitch, a, (fn.t % a.tiles_x) * G::TW,
                      (fn.t / a.tiles_x) * TH);
         }
         if constexpr (VBOX) {
@@ -291,7 +292,7 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
 
             uint32_t o[P];
             finish_outputs(a01, a2k, o);
-            store_px_to(a, frame_dst(a, tile), ty0 + ty, tx0 + tx * P, o);
+            store_px_to(a, frame_dst<MULTI>(a, tile), ty0 + ty, tx0 + tx * P, o);
         }
         if (next >= a.tiles_total) break;
         __syncthreads();
@@ -299,6 +300,16 @@ __global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs 
         __syncthreads();
         tile = next;
     }
+}
+
+template <int R, int WAVES, bool FMA, int P, int NE = 1536, bool SAT = false>
+__global__ __launch_bounds__(WAVES * 64) void adaptive_kernel(const StencilArgs a) {
+    adaptive_body<R, WAVES, FMA, P, NE, SAT, false>(a);
+}
+// multi-frame launches (vip_adaptive_run_rows_batch, radius <= kBatchMaxRadius)
+template <int R, int WAVES, bool FMA, int P, int NE = 1536, bool SAT = false>
+__global__ __launch_bounds__(WAVES * 64) void adaptive_frames_kernel(const StencilArgs a) {
+    adaptive_body<R, WAVES, FMA, P, NE, SAT, true>(a);
 }
 
 #ifndef VIP_ADA_SHORT_LUT
@@ -323,12 +334,24 @@ static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     static_assert(LDS <= kLdsBudget, "adaptive tile does not fit LDS");
     auto kern = adaptive_kernel<R, WAVES, FMA, P, NE, SAT>;
     static std::atomic<unsigned long long> attr_devs{0};
-    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs, SAT)) return rc;
+    const bool multi = a.nframes > 1;
+    if constexpr (R <= kBatchMaxRadius) {
+        if (multi) {
+            kern = adaptive_frames_kernel<R, WAVES, FMA, P, NE, SAT>;
+            static std::atomic<unsigned long long> attr_devs_frames{0};
+            if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs_frames, SAT))
+                return rc;
+        }
+    } else {
+        if (multi) return VIP_ERR_INVALID_ARGUMENT;  // no multi-frame form (the batch entry point loops frames)
+    }
+    if (!multi)
+        if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs, SAT)) return rc;
     note_launch(reinterpret_cast<const void*>(kern));
     StencilArgs args = a;
     args.tiles_x = (a.width + G::TW - 1) / G::TW;
     args.tiles_frame = args.tiles_x * ((a.out_rows + TH - 1) / TH);
-    args.tiles_total = args.tiles_frame * (a.nframes < 1 ? 1 : a.nframes);
+    args.tiles_total = args.tiles_frame * (multi ? a.nframes : 1);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);

@@ -74,9 +74,11 @@ struct FoldRank {  // table index of tap (|ky|, |kx|)
 #else
 #define VIP_BIL_WPE_ATTR
 #endif
-template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false, int TPR = 16,
-          bool SAT = false>
-__global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(const StencilArgs a) {
+// The kernel body; MULTI: a multi-frame launch (bilateral_frames_kernel), whose tiles run
+// from one frame into the next (StencilArgs::nframes). The one-frame kernel compiles with
+// MULTI = false, to exactly the code it had before multi-frame launches existed.
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE, bool FOLD, int TPR, bool SAT, bool MULTI>
+__device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
     using G = Geom<R, P, TPR>;
     constexpr int NT = WAVES * 64;
     constexpr int TH = WAVES * G::RPW;
@@ -116,9 +118,9 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
     // multi-frame launches (plain filter only: guide == src): frame f's tiles follow
     // frame f - 1's, so a workgroup's next tile may be the next frame's
     {
-        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
         const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
-        pg.issue(JOINT ? a.guide : frame_ptr(a.fsrc, a.guide, ft.f), a.guide_pitch, a, tx0, ty0);
+        pg.issue(JOINT ? a.guide : frame_src<MULTI>(a.guide, ft.f), a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
     }
     ls.store(SAT ? lds + SL::T / 4 : lut);
@@ -128,13 +130,13 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
 
     for ([[maybe_unused]] int it = 0;; ++it) {
         VIP_STAMP(it, 0);
-        const FrameTile ft = frame_tile(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
         const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
         if (next < a.tiles_total) {  // next tile's HBM reads fly under this tile's taps
-            const FrameTile fn = frame_tile(a, xcd_tile(next, a.tiles_total));
+            const FrameTile fn = frame_tile<MULTI>(a, xcd_tile(next, a.tiles_total));
             const int nx0 = (fn.t % a.tiles_x) * G::TW, ny0 = (fn.t / a.tiles_x) * TH;
-            pg.issue(JOINT ? a.guide : frame_ptr(a.fsrc, a.guide, fn.f), a.guide_pitch, a, nx0, ny0);
+            pg.issue(JOINT ? a.guide : frame_src<MULTI>(a.guide, fn.f), a.guide_pitch, a, nx0, ny0);
             if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
         }
         if (ty0 + wave * G::RPW < a.out_rows) {  // wave-uniform: skip rows past the frame
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
 
             uint32_t o[P];
             finish_outputs<P, VIP_BIL_RCP != 0>(a01, a2k, o);
-            store_px_to(a, JOINT ? a.dst : frame_dst(a, tile), ty0 + ty, tx0 + tx * P, o);
+            store_px_to(a, JOINT ? a.dst : frame_dst<MULTI>(a, tile), ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);
         if (next >= a.tiles_total) {
@@ -198,6 +200,18 @@ __global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(
         VIP_STAMP(it, 2);
         tile = next;
     }
+}
+
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false, int TPR = 16,
+          bool SAT = false>
+__global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_kernel(const StencilArgs a) {
+    bilateral_body<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT, false>(a);
+}
+// multi-frame launches (vip_bilateral_run_rows_batch; plain filter, radius <= kBatchMaxRadius)
+template <int R, int WAVES, bool JOINT, bool FMA, int COPIES, int P, int NE = 768, bool FOLD = false, int TPR = 16,
+          bool SAT = false>
+__global__ __launch_bounds__(WAVES * 64) VIP_BIL_WPE_ATTR void bilateral_frames_kernel(const StencilArgs a) {
+    bilateral_body<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT, true>(a);
 }
 
 // The joint kernel holds two tile planes; when the full 32-copy LUT leaves room for
@@ -370,12 +384,24 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     static_assert(!SAT || TPR == 16, "SAT: 128-pixel tiles");
     auto kern = bilateral_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT>;
     static std::atomic<unsigned long long> attr_devs{0};
-    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs, SAT)) return rc;
+    const bool multi = !JOINT && a.nframes > 1;
+    if constexpr (!JOINT && !FOLD && R <= kBatchMaxRadius) {
+        if (multi) {
+            kern = bilateral_frames_kernel<R, WAVES, JOINT, FMA, COPIES, P, NE, FOLD, TPR, SAT>;
+            static std::atomic<unsigned long long> attr_devs_frames{0};
+            if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs_frames, SAT))
+                return rc;
+        }
+    } else {
+        if (multi) return VIP_ERR_INVALID_ARGUMENT;  // no multi-frame form (the batch entry point loops frames)
+    }
+    if (!multi)
+        if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), LDS, attr_devs, SAT)) return rc;
     note_launch(reinterpret_cast<const void*>(kern));
     StencilArgs args = a;
     args.tiles_x = (a.width + G::TW - 1) / G::TW;
     args.tiles_frame = args.tiles_x * ((a.out_rows + TH - 1) / TH);
-    args.tiles_total = args.tiles_frame * (JOINT || a.nframes < 1 ? 1 : a.nframes);  // the joint filter: one frame
+    args.tiles_total = args.tiles_frame * (multi ? a.nframes : 1);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);

@@ -522,7 +522,7 @@ int vip_bilateral_run_rows_batch(vip_bilateral_t h, int n, const uint8_t* const*
         return VIP_ERR_INVALID_ARGUMENT;
     if (const int rc = check_batch(n, d_srcs, d_dsts)) return rc;
     const hipStream_t s = (hipStream_t)stream;
-    if (use_runtime_kernel(h->radius)) {  // the runtime-radius kernel: one launch per frame
+    if (use_runtime_kernel(h->radius) || h->radius > kBatchMaxRadius) {  // no multi-frame form: frame by frame
         for (int f = 0; f < n; ++f)
             if (const int rc = vip_bilateral_run_rows(h, d_srcs[f], src_pitch, nullptr, 0, d_dsts[f], dst_pitch,
                                                       out_rows, src_row0, row_lo, row_hi, stream))
@@ -611,7 +611,7 @@ int vip_adaptive_run_rows_batch(vip_adaptive_t h, int n, const uint8_t* const* d
         return VIP_ERR_INVALID_ARGUMENT;
     if (const int rc = check_batch(n, d_srcs, d_dsts)) return rc;
     const hipStream_t s = (hipStream_t)stream;
-    if (use_runtime_kernel(h->radius)) {
+    if (use_runtime_kernel(h->radius) || h->radius > kBatchMaxRadius) {  // no multi-frame form: frame by frame
         for (int f = 0; f < n; ++f)
             if (const int rc = vip_adaptive_run_rows(h, d_srcs[f], src_pitch, d_dsts[f], dst_pitch, out_rows, src_row0,
                                                      row_lo, row_hi, stream))

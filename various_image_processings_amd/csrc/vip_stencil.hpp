@@ -72,6 +72,9 @@ struct SatLut {
 // Frames one launch of the plain bilateral / adaptive kernels may filter (the
 // *_run_rows_batch entry points; a shard's B frames per RCCL group, vip_shard_run_batch).
 constexpr int kMaxBatchFrames = 6;
+// Radii whose plain / adaptive kernels have a multi-frame form (the small-slab radii; a
+// batch of larger radii launches frame by frame)
+constexpr int kBatchMaxRadius = 8;
 
 struct StencilArgs {
     const uint8_t* src;
@@ -692,11 +695,11 @@ __device__ __forceinline__ void finish_outputs(const f2 (&a01)[P], const f2 (&a2
 struct FrameTile {
     int f, t;
 };
+// MULTI = false (every one-frame kernel): tile mt of frame 0, no extra instruction.
+template <bool MULTI>
 __device__ __forceinline__ FrameTile frame_tile(const StencilArgs& a, int mt) {
     int f = 0;
-#ifdef VIP_NO_MULTIFRAME  // measurement builds only: single-frame kernels (batch launches filter frame 0 only)
-    return {f, mt};
-#endif
+    if constexpr (!MULTI) return {f, mt};
     // a one-frame launch has tiles_frame == tiles_total > mt; never loops on tiles_frame <= 0
     while (mt >= a.tiles_frame && a.tiles_frame > 0 && f < kMaxBatchFrames - 1) {
         mt -= a.tiles_frame;
@@ -704,26 +707,39 @@ __device__ __forceinline__ FrameTile frame_tile(const StencilArgs& a, int mt) {
     }
     return {f, mt};
 }
+// Multi-frame kernels take the StencilArgs as their only argument, so it starts the kernel
+// argument segment: frame f's pointer is one scalar load from there (indexing the by-value
+// argument through a reference would copy the whole struct to scratch).
+template <class T>
+__device__ __forceinline__ T kernarg_at(size_t byte_offset) {
+    typedef const __attribute__((address_space(4))) char kchar;
+    typedef const __attribute__((address_space(4))) T kT;
+    kchar* base = (kchar*)__builtin_amdgcn_kernarg_segment_ptr();
+    return *(kT*)(base + byte_offset);
+}
+
 // Output base of launch tile `tile`'s frame, derived again at the store: keeping the frame
 // index live across the tap loop costs scalar registers the loop's spatial weights use
 // (measured +1 % on the 4K r=7 launch).
+template <bool MULTI>
 __device__ __forceinline__ uint8_t* frame_dst(const StencilArgs& a, int tile) {
+    if constexpr (!MULTI) return a.dst;
     __asm__ volatile("" : "+s"(tile));  // recompute here, not from the tile's start
     int mt = xcd_tile(tile, a.tiles_total), f = 0;
     while (mt >= a.tiles_frame && a.tiles_frame > 0 && f < kMaxBatchFrames - 1) {
         mt -= a.tiles_frame;
         ++f;
     }
-    return a.fdst[f];  // one scalar load at the store (kernel arguments), nothing held across the taps
+    // one scalar load at the store, nothing held across the taps
+    return f == 0 ? a.dst : kernarg_at<uint8_t*>(offsetof(StencilArgs, fdst) + f * sizeof(uint8_t*));
 }
 
 // fsrc[f] / fdst[f] by uniform selects (no dynamic index into the kernel arguments)
-template <class T>
-__device__ __forceinline__ T frame_ptr(const T (&p)[kMaxBatchFrames], T p0, int f) {
-#ifdef VIP_NO_MULTIFRAME
-    return p0;
-#endif
-    return f == 0 ? p0 : p[f];  // a scalar load when needed, not four pointers held in SGPRs
+// frame f's source (fsrc[f]; p0 for frame 0)
+template <bool MULTI>
+__device__ __forceinline__ const uint8_t* frame_src(const uint8_t* p0, int f) {
+    if constexpr (!MULTI) return p0;
+    return f == 0 ? p0 : kernarg_at<const uint8_t*>(offsetof(StencilArgs, fsrc) + f * sizeof(const uint8_t*));
 }
 
 // Write P RGB outputs (3P bytes) of row oy starting at column x to dst (A: StencilArgs or
