@@ -434,9 +434,10 @@ def pmc_traffic(config: str, kernels: list, per_step: int = 1):
 
 def launched(kernels: list, prefix: str):
     """The launched kernel (exact name) that starts with prefix, or None; a shared launch's
-    multi-frame form of it (`..._frames_kernel<`, vip_*_run_rows_batch) counts too."""
+    multi-frame form of it (`..._frames_kernel<`, vip_*_run_rows_batch) first when present
+    (it carries the frames then; a partial last batch of one frame uses the other)."""
     frames = prefix.replace("_kernel<", "_frames_kernel<")
-    hit = [k for k in kernels if k.startswith(prefix)] + [k for k in kernels if k.startswith(frames)]
+    hit = [k for k in kernels if k.startswith(frames)] + [k for k in kernels if k.startswith(prefix)]
     return hit[0] if hit else None
 
 
