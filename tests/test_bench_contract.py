@@ -239,3 +239,14 @@ def test_native_trial_forms_keep_buffers_on_one_stream():
     tex = bench.native_forms([2], texture=True, graph=True)
     assert all(not sp and sh is None for _, sp, _, _, sh in tex) and [f for f in tex if f[3]] == [(2, False, 1, True, None)]
     assert len(set(forms)) == len(forms)
+
+
+def test_launched_prefers_the_multi_frame_form():
+    """A shared launch's kernel (`..._frames_kernel<`) names the line's kernel when present;
+    otherwise the one-frame kernel with the prefix; None when neither launched."""
+    one = "void vip::bilateral_kernel<7, 16, false, true, 32, 4, 768, false, 64, false>"
+    frames = "void vip::bilateral_frames_kernel<7, 16, false, true, 32, 4, 768, false, 64, false>"
+    assert bench.launched([one, frames], "void vip::bilateral_kernel<7,") == frames
+    assert bench.launched([one], "void vip::bilateral_kernel<7,") == one
+    assert bench.launched(["void vip::adaptive_kernel<7, 16, true, 4, 512, true>"],
+                          "void vip::bilateral_kernel<7,") is None
