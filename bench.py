@@ -132,47 +132,6 @@ def _run_ranks(n, argv, timeout_s, script, capture):
     return rc, lines
 
 
-GRAPH_ATTEMPT_TIMEOUT_S = 420.0
-
-
-def launch_with_graph_attempt(n: int, argv: list, timeout_s: float = LAUNCH_TIMEOUT_S, script: str | None = None) -> int:
-    """`python bench.py --gpus N` (native exchange): first the run whose split / batch trial
-    also times each frame replayed from a captured hipGraph (--graph: the image's HIP + RCCL
-    loaded before torch, preload_system_rocm); if that run fails or runs out of its own
-    bound, the same measurement without graph capture (--no-graph). Exactly one JSON line
-    is printed, the last one of the run that succeeded, with `graph_attempt` saying what
-    happened. Returns the exit status of the run whose line was printed."""
-    rc, lines = launch_ranks_json(n, list(argv) + ["--graph"], min(timeout_s, GRAPH_ATTEMPT_TIMEOUT_S), script)
-    if rc == 0 and lines:
-        line = json.loads(lines[-1])
-        line["graph_attempt"] = "ok: the trial included the captured form"
-        print(json.dumps(line), flush=True)
-        return 0
-    why = f"the run with graph capture ended with status {rc}" + ("" if lines else " and no line")
-    print(f"bench.py: {why}; measuring again without graph capture", file=sys.stderr, flush=True)
-    rc2, lines2 = launch_ranks_json(n, list(argv) + ["--no-graph"], timeout_s, script)
-    if lines2:
-        line = json.loads(lines2[-1])
-        line["graph_attempt"] = f"failed ({why}); measured without graph capture"
-        print(json.dumps(line), flush=True)
-    return rc2
-
-
-SYSTEM_ROCM = ("/opt/rocm/lib/libamdhip64.so.7", "/opt/rocm/lib/librccl.so.1")
-
-
-def preload_system_rocm() -> None:
-    """--graph: load the image's ROCm HIP runtime and RCCL (7.2 / 2.27.7) into the global
-    symbol scope BEFORE torch, so torch and the library share them. torch's bundled RCCL
-    2.26.6 crashes when an RCCL group is captured into a hipGraph (measured in every capture
-    mode, profiles/r04_graph_capture.txt); the image's RCCL captures and replays correctly
-    (tests/cpp/shard_graph_test). torch's own copies still load beside them (their file
-    names differ), so the process ends with os._exit once its line is printed."""
-    import ctypes
-    for lib in SYSTEM_ROCM:
-        ctypes.CDLL(lib, mode=ctypes.RTLD_GLOBAL)
-
-
 def halo_batches(streams: int) -> list:
     """Frames per RCCL group the N > 1 native path may use with this many streams: frame i
     runs in batch i // B on stream (i // B) % S, so B * S must divide NBUF for buffer
@@ -193,21 +152,30 @@ TRIAL_STREAMS = (2, 3, 4)
 SHARED_FREE_CUS = (0, 8, 16, 24, 32)
 
 
-def native_forms(stream_counts, texture: bool, graph: bool) -> list:
-    """The N > 1 native trial's forms (S streams, split, B frames per RCCL group, graph,
-    shared): every S with each B that keeps a buffer on one stream (halo_batches), the split /
-    one-launch pair (the texture filter has no split), with `graph` one captured form per
-    (S, split), and for B > 1 after the exchange the B frames in shared launches
-    (vip_shard_set_frames_launch; plain and adaptive filters) leaving each of SHARED_FREE_CUS
-    CUs free. shared is None for one launch per frame, else that free-CU count."""
+def native_forms(stream_counts, texture: bool, batches=None) -> list:
+    """The N > 1 native trial's forms (S streams, split, B frames per RCCL group, shared):
+    every S with each B that keeps a buffer on one stream (halo_batches; only `batches` when
+    given), the split / one-launch pair (the texture filter has no split), and for B > 1
+    after the exchange the B frames in shared launches (vip_shard_set_frames_launch; plain
+    and adaptive filters) leaving each of SHARED_FREE_CUS CUs free. shared is None for one
+    launch per frame, else that free-CU count. No captured-graph form: graph replay needs
+    RCCL >= 2.27.7 and torch binds its own 2.26.6 (vip_shard_set_graph refuses it); it is a
+    C/C++ feature (tests/cpp/shard_graph_test)."""
     forms = []
     for n in stream_counts:
+        bs = [b for b in halo_batches(n) if batches is None or b in batches]
         for split in ((False,) if texture else (True, False)):
-            forms += [(n, split, b, False, None) for b in halo_batches(n)]
-            forms += [(n, split, 1, True, None)] if graph else []
+            forms += [(n, split, b, None) for b in bs]
             if not split and not texture:
-                forms += [(n, split, b, False, fc) for b in halo_batches(n) if b > 1 for fc in SHARED_FREE_CUS]
+                forms += [(n, split, b, fc) for b in bs if b > 1 for fc in SHARED_FREE_CUS]
     return forms
+
+
+def single_gpu_forms(stream_counts, batches=None) -> list:
+    """The N = 1 trial's forms for the plain and adaptive filters, the same (S, B) grid as
+    the N > 1 trial so both lines are timed in the same forms: S streams of frames in
+    flight, B frames per shared launch (vip_*_run_rows_batch; B = 1 one launch per frame)."""
+    return [(n, b) for n in stream_counts for b in halo_batches(n) if batches is None or b in batches]
 
 
 BASELINE_METRIC = "Mpixels/sec bilateral r=7 on 4K RGB; % HBM roofline; 1/2/4/8-GPU scaling"
@@ -233,7 +201,10 @@ CONFIGS = {
                workload="adaptive bilateral r=7 3840x2160 RGB8"),
     "c4": dict(kind="texture", width=3840, rows_per_rank=2160, ksize=5, nitr=5,
                workload="bilateral texture k=5 nitr=5 3840x2160 RGB8"),
-    "c5": dict(kind="bilateral", width=16384, frame_height=16384, ksize=31,
+    # c5 at N = 1: one 805 MB frame per launch (4 rounds of 256 workgroups over 8,192 tiles), so
+    # sharing a launch between frames cannot remove a tail worth timing; the N = 1 trial keeps
+    # 2 streams and one frame per launch
+    "c5": dict(kind="bilateral", width=16384, frame_height=16384, ksize=31, single_gpu_forms=[(2, 1)],
                workload="bilateral r=15 16384x16384 RGB8 row-tiled"),
     # not a BASELINE config: the largest ksize the reference runs (its shared memory
     # fits CUDA's 48 KB default up to 65), on the runtime-radius kernel
@@ -299,15 +270,12 @@ def parse():
     p.add_argument("--rehearse-native", action="store_true")
     # with --rehearse-native: this rank's slab of an N-way row split, whose two row neighbours
     # are the rank itself over a one-rank RCCL communicator (vip_shard_create_loopback), so
-    # the real exchange, its trial forms and graph replay run on one GPU. One rank's slab:
-    # not a scaling number.
+    # the real exchange and its trial forms run on one GPU. One rank's slab: not a scaling
+    # number.
     p.add_argument("--loopback", type=int, default=0, metavar="N")
-    # N > 1 native: also time each frame replayed from a captured hipGraph (vip_shard_set_graph)
-    # in the split / batch trial; loads the image's HIP runtime and RCCL before torch
-    # (preload_system_rocm)
-    # default: off inside a rank; `python bench.py --gpus N` (native exchange) first tries a
-    # run with it and falls back to one without (launch_with_graph_attempt)
-    p.add_argument("--graph", action=argparse.BooleanOptionalAction, default=None)
+    # frames per shared launch (N = 1) / per RCCL group (N > 1): fixes B in the trial
+    # (default: the trial picks from halo_batches(S))
+    p.add_argument("--batch", type=int, default=None, choices=[1, 2, 3, 4, 6])
     # --gpus N > 1 without WORLD_SIZE in the environment: this process starts the N ranks
     # itself (a child torchrun) and ends them after this many seconds
     p.add_argument("--launch-timeout", type=float, default=LAUNCH_TIMEOUT_S)
@@ -418,6 +386,27 @@ def pmc_summary(config: str, kernel, need: str):
     return None, None
 
 
+def isolated_sample(config: str, kernel) -> dict | None:
+    """The committed single-stream launch-duration sample of exactly this kernel: the newest
+    profiles/r*_<config>_isolated.csv (scripts/isolated_sample.py over a rocprofv3
+    --kernel-trace of `bench.py --streams 1 --batch 1`, one row per launch of the last
+    launches of each kernel, none overlapping another) that holds it. The roofline's live
+    launch time sits beside it; None when no sample names this instantiation."""
+    import csv
+    import glob
+    import statistics
+    if not kernel:
+        return None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_isolated.csv")), reverse=True):
+        with open(f) as fh:
+            ns = [int(r["duration_ns"]) for r in csv.DictReader(fh) if r["kernel"] == kernel]
+        if ns:
+            return dict(source=os.path.relpath(f, ROOT), launches=len(ns), mean_us=round(sum(ns) / len(ns) / 1e3, 2),
+                        median_us=round(statistics.median(ns) / 1e3, 2), min_us=round(min(ns) / 1e3, 2),
+                        max_us=round(max(ns) / 1e3, 2))
+    return None
+
+
 def pmc_traffic(config: str, kernels: list, per_step: int = 1):
     """HBM bytes per launch of these exact kernels from the committed PMC summaries
     (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, scripts/pmc_summary.py).
@@ -483,14 +472,14 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms,
         jbf = dict(kernel=f"joint bilateral_kernel<R={rj}> (ksize {2 * k - 1}, {taps} taps)", avg_launch_ms=round(j_ms, 4),
                    bound="valu-fp32", achieved=round(jbf_tf, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                    frac=round(jbf_tf / PEAK_FP32_TFLOPS, 4), flop_per_px=8 * taps,
-                   valu_issue=valu_issue(config, jbf_k, j_ms))
+                   valu_issue=valu_issue(config, jbf_k, j_ms), isolated_sample=isolated_sample(config, jbf_k))
         g_gbs = 6.0 * px / (g_ms * 1e-3) / 1e9  # reads the frame, writes the guide
         gtraffic, gsrc = pmc_traffic(config, [guide_k])
         guide = dict(kernel="texture_guide_fused_kernel (gradient + blur/mRTV + argmin/alpha guide, fused)",
                      avg_launch_ms=round(g_ms, 4), bound="valu-issue", bytes_per_px=6,
                      hbm=dict(achieved=round(g_gbs, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(g_gbs / PEAK_HBM_GBS, 4),
                               traffic=gtraffic, traffic_source=gsrc),
-                     valu_issue=valu_issue(config, guide_k, g_ms))
+                     valu_issue=valu_issue(config, guide_k, g_ms), isolated_sample=isolated_sample(config, guide_k))
         dom, other = (jbf, guide) if j_ms >= g_ms else (guide, jbf)
         if dom is jbf:
             jtraffic, jsrc = pmc_traffic(config, [jbf_k])
@@ -644,11 +633,47 @@ def native_shards(args, cfg, frame_h, rank, world, n):
     return shards, None
 
 
+def rccl_evidence(shards, rank, world, expected_count) -> dict:
+    """What RCCL itself reports about the communicators this run exchanged over: every
+    rank's ncclCommCount / ncclCommUserRank / ncclCommCuDevice (vip_shard_comm_info, for each
+    of its shards, one per stream) and its device's PCI bus id, gathered to every rank over
+    the control process group. `problems` lists what would make an N-GPU line not an N-GPU
+    measurement: a communicator of another size, a rank that is not its own user rank, or
+    two ranks on one device."""
+    import torch.distributed as dist
+
+    from various_image_processings_amd.sharded import rccl_version
+    infos = [s.comm_info() for s in shards]
+    mine = dict(rank=rank, count=infos[0]["count"], user_rank=infos[0]["user_rank"], device=infos[0]["device"],
+                pci_bus_id=infos[0]["pci_bus_id"], shards=len(infos),
+                shards_agree=all((i["count"], i["user_rank"], i["device"]) ==
+                                 (infos[0]["count"], infos[0]["user_rank"], infos[0]["device"]) for i in infos))
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
+    counts = sorted({r_["count"] for r_ in ranks})
+    buses = [r_["pci_bus_id"] for r_ in ranks]
+    problems = []
+    if counts != [expected_count]:
+        problems.append(f"communicator sizes {counts}, expected {expected_count}")
+    if expected_count > 1 and any(r_["user_rank"] != r_["rank"] for r_ in ranks):
+        problems.append("a rank's RCCL user rank differs from its process rank")
+    if not all(r_["shards_agree"] for r_ in ranks):
+        problems.append("a rank's communicators (one per stream) disagree")
+    if len(set(buses)) != len(buses):
+        problems.append(f"{len(buses)} ranks on {len(set(buses))} distinct devices")
+    return dict(ranks=ranks, count=counts[0] if len(counts) == 1 else counts, distinct_devices=len(set(buses)),
+                rccl_version=rccl_version(),
+                problems=problems)
+
+
 def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms=None):
     """Build one workload (buffers, handles) and time it: W warm-up steps, then K steps
     between barriers + device syncs, max over ranks. Returns the measured quantities.
-    s_forms: the stream counts the N > 1 native trial may pick from (at most len(streams));
-    default: all the streams."""
+    s_forms: the stream counts the trial may pick from (at most len(streams)); default: all
+    the streams."""
     import torch.distributed as dist
 
     from various_image_processings_amd.filters import _TextureImpl, launched_kernels
@@ -664,6 +689,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     gen.manual_seed(42 + rank)
     res = dict(frame_h=frame_h, exchange=None, stage_ms=None, samples=None)
     native = False
+    single_batch = False  # N = 1 plain / adaptive: the trial may share launches between frames
     cdev = dev if state.get("backend") == "nccl" else "cpu"  # control tensors of the process group
     multi = state.get("multi", world > 1)  # a process group is up (N > 1, or --rehearse-native)
 
@@ -700,6 +726,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         native = shards is not None
         if native:
             sb = shards[0]
+            # RCCL's own account of the communicators (checked into the line's "valid")
+            res["rccl"] = rccl_evidence(shards, rank, world, 1 if args.loopback > 1 else world)
         elif cfg["kind"] == "texture":
             # torch P2P: one halo exchange of nitr * texture_halo_rows(k) rows per frame,
             # then shrinking ghost zones (sharded.ShardedTexture; one per stream: it owns
@@ -729,6 +757,11 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
 
             def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
                 launch(sp[i % NBUF], dp[i % NBUF], sraw[h])
+            if not multi:
+                # N = 1: B frames in one shared launch (vip_*_run_rows_batch, all CUs), the
+                # form the N > 1 line may pick after its exchange
+                single_batch = True
+                nbatches = [sb.batch_launcher()] * len(streams)
     has_peers = world > 1 or (native and args.loopback > 1)
     res["exchange"] = (None if not multi else
                        ("native vip_shard (RCCL ncclSend/ncclRecv with the row neighbours; one communicator per "
@@ -744,10 +777,12 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     # native -- vip_shard_run_timed's run start, halos in, interior done, edges done.
     marks = []
     group = state.get("torch_group")
-    # native N > 1: frames may share one RCCL group per B frames (vip_shard_run_batch; the
-    # group's cost is mostly fixed, profiles/r03_rccl_enqueue.txt). Frame i then runs on
-    # stream (i // B) % S; B * S divides NBUF, so buffer i % NBUF still always meets the
-    # same stream and a halo receive into it stays ordered after its last reader.
+    # frames may share one RCCL group (N > 1 native, vip_shard_run_batch; the group's cost is
+    # mostly fixed, profiles/r03_rccl_enqueue.txt) or one launch (N = 1, vip_*_run_rows_batch)
+    # per B frames. Frame i then runs on stream (i // B) % S; B * S divides NBUF, so buffer
+    # i % NBUF still always meets the same stream and a halo receive into it stays ordered
+    # after its last reader.
+    batching = native or single_batch
     s_forms = list(s_forms or [S])
     hb = dict(B=1, S=s_forms[0], pending=[])  # S: the streams in use (the trial may change it)
 
@@ -762,14 +797,14 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # (S divides NBUF), so a halo receive into it is ordered after its last reader
         h = 0 if sample else i % hb["S"]
         s = streams[h]
-        if native and not sample and hb["B"] > 1:
+        if batching and not sample and hb["B"] > 1:
             # batches end on multiples of B (a phase end flushes a partial one), so every
             # frame of a batch has the same i // B, hence the same stream
             hb["pending"].append(i)
             if (i + 1) % hb["B"] == 0:
                 flush()
             return
-        if native and sample:
+        if batching and sample:
             flush()
         if not multi and not sample:  # one GPU: the launch names its stream; no torch stream context
             run(i, s, h)
@@ -819,6 +854,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             step(i_settle)
             i_settle += 1
         torch.cuda.synchronize(dev)
+    batches = None if args.batch is None else [args.batch]
     if native and not has_peers:
         # one rank (--rehearse-native): no halo moves, so split / batch forms would only
         # time noise between identical launches; keep the defaults and say so
@@ -831,21 +867,19 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # Which is faster depends on the exchange's latency and host cost on this machine:
         # time each (max over ranks) and keep the fastest. The texture filter has no split
         # (every iteration reads the halo region).
-        # Graph mode (vip_shard_set_graph, one frame per captured graph, B = 1) replays each
-        # (buffer, stream)'s exchange + launches with one hipGraphLaunch: the per-frame host
-        # cost of an RCCL group (16-30 us, profiles/r03_rccl_enqueue.txt) against a rank's
-        # ~25 us C2 launch at N = 8 is what it removes.
         # With several stream counts (TRIAL_STREAMS), S is a trial dimension too: frames in
         # flight hide one stream's exchange latency behind the others' launches.
         trial = {}
         n_trial = 48  # a multiple of every B
-        for n_s, split, b, graph, shared in native_forms(s_forms, cfg["kind"] == "texture", bool(args.graph)):
+        forms = native_forms(s_forms, cfg["kind"] == "texture", batches)
+        if not forms:
+            raise SystemExit(f"bench.py: --batch {args.batch} fits none of the stream counts {s_forms}")
+        for n_s, split, b, shared in forms:
             for x in shards:
                 x.set_split(split)
-                x.set_graph(graph)
                 x.set_frames_launch(shared is not None, shared or 0)
             hb["B"], hb["S"] = b, n_s
-            for _ in range(NBUF):  # untimed: captures every (buffer, stream) graph in graph mode
+            for _ in range(NBUF):  # untimed: every (buffer, stream) pair once in this form
                 step(i_settle)
                 i_settle += 1
             flush()
@@ -860,12 +894,11 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             dist.barrier()
             dt = torch.tensor([(time.perf_counter() - t0) / n_trial * 1e3], dtype=torch.float64, device=cdev)
             dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-            trial[(n_s, split, b, graph, shared)] = float(dt[0])
-        best_s, best_split, best_b, best_graph, best_shared = min(trial, key=trial.get)
+            trial[(n_s, split, b, shared)] = float(dt[0])
+        best_s, best_split, best_b, best_shared = min(trial, key=trial.get)
         res["split_on"] = best_split
         for x in shards:
             x.set_split(best_split)
-            x.set_graph(best_graph)
             x.set_frames_launch(best_shared is not None, best_shared or 0)
         hb["B"], hb["S"] = best_b, best_s
         res["streams"] = best_s
@@ -875,23 +908,51 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             res["exchange"] += f"; the halos of {best_b} frames per RCCL group"
             if best_shared is not None:
                 res["exchange"] += ", filtered in one launch" + (f" leaving {best_shared} CUs free" if best_shared else "")
-        if best_graph:
-            res["exchange"] += "; each frame replayed from a captured hipGraph"
         res["split"] = dict(chosen="interior rows during the exchange, then the edge bands" if best_split
                             else "one launch after the exchange",
-                            graph=best_graph, frames_launch=best_shared,
+                            frames_launch=best_shared,
                             trial_ms_per_step={(f"s{s_}_" if len(s_forms) > 1 else "")
                                                + ("split" if sp_ else "one_launch") + (f"_batch{b_}" if b_ > 1 else "")
-                                               + ("_graph" if g_ else "")
                                                + ("" if sh_ is None else "_one_kernel" + (f"_free{sh_}" if sh_ else "")):
                                                round(v, 4)
-                                               for (s_, sp_, b_, g_, sh_), v in trial.items()})
+                                               for (s_, sp_, b_, sh_), v in trial.items()})
         res["halo_batch"] = best_b
+    elif single_batch:
+        # N = 1, the same (S, B) grid as the N > 1 trial: S frames in flight, B frames per
+        # shared launch. Each form runs as many steps as fill about a quarter of the timed
+        # region (a multiple of every B) after one untimed pass over the buffers; keep the
+        # fastest.
+        trial = {}
+        n_trial = 6 * max(8, args.steps // 24)
+        forms = [f for f in cfg.get("single_gpu_forms", single_gpu_forms(s_forms, batches))
+                 if f[0] <= len(streams) and (batches is None or f[1] in batches)] or single_gpu_forms(s_forms, batches)
+        if not forms:
+            raise SystemExit(f"bench.py: --batch {args.batch} fits none of the stream counts {s_forms}")
+        for n_s, b in forms:
+            hb["B"], hb["S"] = b, n_s
+            for _ in range(NBUF):
+                step(i_settle)
+                i_settle += 1
+            flush()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(n_trial):
+                step(i_settle)
+                i_settle += 1
+            flush()
+            torch.cuda.synchronize(dev)
+            trial[(n_s, b)] = (time.perf_counter() - t0) / n_trial * 1e3
+        best_s, best_b = min(trial, key=trial.get)
+        hb["B"], hb["S"] = best_b, best_s
+        res["streams"] = best_s
+        res["batch"] = dict(chosen=best_b, trial_steps=n_trial,
+                            trial_ms_per_step={f"s{s_}_batch{b_}": round(v, 4) for (s_, b_), v in trial.items()})
     res["settle_steps"] = i_settle
+    S_run = hb["S"]  # streams the timed steps use
     base = i_settle
     for i in range(args.warmup):
         step(base + i)
-    if native:
+    if batching:
         flush()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -901,15 +962,15 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     launched_kernels()  # the line names the kernels of the timed steps (not of the settle's first launches)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for s in streams[1:]:
+    for s in streams[1:S_run]:
         s.wait_event(ev0)
     for i in range(args.steps):
         step(base + args.warmup + i)
-    if native:
+    if batching:
         flush()  # a partial last batch is part of the timed frames
     host_s = time.perf_counter() - t0  # every step enqueued
     res["kernels_timed"] = launched_kernels()
-    for s in streams[1:]:
+    for s in streams[1:S_run]:
         stream.wait_stream(s)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
@@ -920,6 +981,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     after = base + args.warmup + args.steps
     single_ms = None
     parts = None
+    B = hb["B"]
+    res["frames_in_flight"] = S_run * B
     if multi:
         for i in range(max(4, args.steps // 4)):
             step(after + i, sample=True)
@@ -933,45 +996,77 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             else:
                 parts = dict(exchange_ms=avg(0, 1), wait_ms=avg(0, 2), filter_ms=avg(2, 3), run_ms=avg(0, 3))
             kernel_ms = parts["run_ms"]
+            if B > 1 and has_peers:
+                # one frame's latency in the chosen form: a whole group of B frames (one RCCL
+                # group, then its launches) alone on one stream, from the point its own rows
+                # are written to the last output row -- what the last frame of a group waits
+                lat = []
+                j0 = after + max(4, args.steps // 4)
+                j0 += (-j0) % B
+                for g_ in range(max(2, args.steps // (4 * B))):
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    nbatches[0]([sp[(j0 + g_ * B + f) % NBUF] for f in range(B)],
+                                [dp[(j0 + g_ * B + f) % NBUF] for f in range(B)], sraw[0])
+                    e1.record(stream)
+                    lat.append((e0, e1))
+                torch.cuda.synchronize(dev)
+                parts["group_latency_ms"] = sum(a.elapsed_time(b) for a, b in lat) / len(lat)
         else:
             parts = dict(exchange_ms=avg(0, 1), kernel_ms=avg(1, 2))
             kernel_ms = parts["kernel_ms"]
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
-        if S > 1:
+        if S_run > 1 or B > 1:
             # the roofline is per kernel: its launch duration comes from max(4, K/4) more
-            # frames on ONE stream, back to back, after the timed region (the S-stream
-            # launches overlap, so their event spans are not launch durations)
+            # frames (a multiple of B) on ONE stream, back to back, after the timed region
+            # (the S-stream launches overlap, so their event spans are not launch durations;
+            # with B > 1 one launch carries B frames and the duration is per frame)
             n1 = max(4, args.steps // 4)
+            n1 += (-n1) % B
             timed_kernels = set(res["kernels_timed"])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            for i in range(n1):
-                run(after + i)
-            e1.record(stream)
-            torch.cuda.synchronize(dev)
-            single_ms = e0.elapsed_time(e1) / n1
+
+            def one_stream(first):
+                e0.record(stream)
+                if B > 1:
+                    for j in range(first, first + n1, B):
+                        nbatches[0]([sp[(j + f) % NBUF] for f in range(B)], [dp[(j + f) % NBUF] for f in range(B)],
+                                    sraw[0])
+                else:
+                    for i in range(n1):
+                        run(first + i)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                return e0.elapsed_time(e1) / n1
+
+            single_ms = one_stream(after + (-after) % B)
             if not set(launched_kernels()) <= timed_kernels:
                 # one stream made the library pick another tiling than the frames in flight
                 # did (its small-frame tiling counts the streams in use): time the timed
                 # region's kernel, back to back on one stream, with the frame count forced
                 # to the S the timed frames had (vip_bilateral_set_frames_in_flight)
                 import various_image_processings_amd as vip_
-                vip_.set_bilateral_frames_in_flight(min(S, 4))
+                vip_.set_bilateral_frames_in_flight(min(S_run, 4))
                 try:
-                    e0.record(stream)
-                    for i in range(n1):
-                        run(after + n1 + i)
-                    e1.record(stream)
-                    torch.cuda.synchronize(dev)
+                    single_ms = one_stream(after + n1 + (-(after + n1)) % B)
                 finally:
                     vip_.set_bilateral_frames_in_flight(0)
-                single_ms = e0.elapsed_time(e1) / n1
-                res["launch_timing"] = (f"one stream, the tiling planned for the timed region's {S} frames in flight "
-                                        f"(vip_bilateral_set_frames_in_flight)")
+                res["launch_timing"] = (f"one stream, the tiling planned for the timed region's {S_run} frames in "
+                                        f"flight (vip_bilateral_set_frames_in_flight)")
                 if not set(launched_kernels()) <= timed_kernels:
                     res["launch_timing"] += "; WARNING: another kernel ran"
+            if B > 1:
+                res["launch_timing"] = (res.get("launch_timing", "one stream") +
+                                        f"; {B} frames per launch, duration per frame")
     launch_ms = single_ms if single_ms is not None else kernel_ms
+    # one frame's latency: the whole launch that carries it on an idle stream (N = 1) or
+    # its RCCL group's exchange and launches (N > 1); the reference's public call blocks for
+    # one frame (sample/benchmark/main.cpp:20-33 times one call per frame)
+    if not multi:
+        res["frame_latency_ms"] = launch_ms * B
+    elif parts:
+        res["frame_latency_ms"] = parts.get("group_latency_ms", parts.get("run_ms", kernel_ms))
     fused = cfg["kind"] == "texture" and world == 1 and not args.loopback and args.texture_mode == "fused"
     if cfg["kind"] == "texture" and world == 1 and not args.loopback and not fused:
         # Per-stage split of the frame: an event between two launches costs a few us of
@@ -988,12 +1083,15 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         per = launch_ms / nit
         res["stage_ms"] = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
                            "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
-    keys = ["elapsed", "launch", "host"] + (sorted(parts) if parts else [])
-    vals = [elapsed, launch_ms, host_s] + ([parts[x] for x in sorted(parts)] if parts else [])
+    keys = ["elapsed", "launch", "host", "latency"] + (sorted(parts) if parts else [])
+    vals = [elapsed, launch_ms, host_s, res.get("frame_latency_ms", 0.0)] + \
+        ([parts[x] for x in sorted(parts)] if parts else [])
     t = torch.tensor(vals, dtype=torch.float64, device=cdev)
     if multi:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     got = dict(zip(keys, (float(v) for v in t)))
+    if "frame_latency_ms" in res:
+        res["frame_latency_ms"] = got["latency"]
     # every kernel instantiation this workload launched (N = 1 with S > 1 streams: those of the
     # timed frames)
     res["kernels"] = res.pop("kernels_timed")
@@ -1004,7 +1102,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         for x in shards:
             x.close()
     res.update(elapsed=got["elapsed"], launch_ms=got["launch"], host_s=got["host"], frame_ms=kernel_ms, rows=rows, geo=geo,
-               parts={x: got[x] for x in sorted(parts)} if parts else None, native=native, fused=fused)
+               parts={x: got[x] for x in sorted(parts)} if parts else None, native=native, fused=fused, batch=B,
+               **({"batch_trial": res["batch"]} if isinstance(res.get("batch"), dict) else {}))
     return res
 
 
@@ -1015,12 +1114,8 @@ def main():
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.rehearse_native:
         # plain `python bench.py --gpus N`: start the N ranks (nothing has touched the GPU)
-        native = args.exchange in (None, "native") and not args.same_device and args.backend != "gloo"
-        if args.graph is None and native:
-            sys.exit(launch_with_graph_attempt(args.gpus, sys.argv[1:], args.launch_timeout))
+        # one run, one HIP runtime and one RCCL per rank (torch's): no graph form, no retry
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
-    if args.graph:
-        preload_system_rocm()
     import torch
     import torch.distributed as dist
 
@@ -1082,9 +1177,11 @@ def main():
     sharded = gw > 1  # this process filters a slab of a larger frame
     frame_h = cfg.get("frame_height") or (per_rank * gw if args.scaling == "weak" else per_rank)
     s_forms = None
-    if sharded and args.exchange == "native" and not fixed_streams:
-        # N > 1 native: the trial also picks the frames in flight (TRIAL_STREAMS), one
-        # shard per stream
+    if not fixed_streams and ((sharded and args.exchange == "native") or
+                              (not state["multi"] and cfg["kind"] in FLOP_PER_TAP)):
+        # the trial also picks the frames in flight (TRIAL_STREAMS): at N > 1 native one
+        # shard per stream; at N = 1 (plain and adaptive filters) the same S x B grid, so
+        # the N = 1 and N > 1 lines are timed in the same forms
         s_forms = list(TRIAL_STREAMS)
         streams += [torch.cuda.Stream(dev) for _ in range(max(s_forms) - len(streams))]
     m = measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms)
@@ -1119,7 +1216,12 @@ def main():
         # the committed PMC summaries are single-GPU whole-frame launches
         # the exact instantiation this run launched (vip_launched_kernels), for the PMC lookup
         kname = launched(m["kernels"], cfg.get("kernel", f"void vip::{cfg['kind']}_kernel<{r},"))
+        # a shared launch (vip_*_run_rows_batch, B > 1) carries B frames: its per-launch PMC
+        # counts (collected in the same form) are divided by B to match the per-frame duration
+        fpl = m["batch"] if kname and "_frames_kernel<" in kname else 1
         traffic, tsrc = (None, None) if sharded else pmc_traffic(args.config, [kname])
+        if traffic:
+            traffic /= fpl
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
@@ -1130,11 +1232,14 @@ def main():
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
                              bytes_per_px=6))
         if not sharded:  # the committed PMC summaries are whole-frame launches
-            roof["valu_issue"] = valu_issue(args.config, kname, launch_ms)
-            if len(streams) > 1:  # the chip's rate with S frames in flight (launches overlap)
+            roof["valu_issue"] = valu_issue(args.config, kname, launch_ms * fpl)
+            if fpl > 1:
+                roof["frames_per_launch"] = fpl
+            roof["isolated_sample"] = isolated_sample(args.config, kname)
+            if m["frames_in_flight"] > 1:  # the chip's rate with frames in flight (launches overlap)
                 fl = flops / (ms_per_step * 1e-3) / 1e12
                 roof["in_flight"] = dict(achieved=round(fl, 3), frac=round(fl / PEAK_FP32_TFLOPS, 4), unit="TFLOP/s",
-                                         note=f"{len(streams)} frames in flight: flops per frame / ms_per_step")
+                                         note=f"{m['frames_in_flight']} frames in flight: flops per frame / ms_per_step")
         else:
             roof["avg_launch_note"] = ("per-rank device time of one step on one stream: "
                                        + ("vip_shard_run (exchange, then the own rows: "
@@ -1174,14 +1279,33 @@ def main():
         # frames in flight on S streams (step i on stream i % S); at N=1 and S>1 the
         # timed region's device time per frame, all streams together
         "streams": m.get("streams", S),
-        **({"frame_ms_in_flight": round(m["frame_ms"], 4)} if world == 1 and S > 1 else {}),
+        # S streams x B frames per shared launch (N = 1) or per RCCL group (N > 1)
+        "frames_in_flight": m["frames_in_flight"],
+        **({"frame_latency_ms": round(m["frame_latency_ms"], 4)} if m.get("frame_latency_ms") else {}),
+        **({"frame_ms_in_flight": round(m["frame_ms"], 4)} if world == 1 and m["frames_in_flight"] > 1 else {}),
         "settle": {"seconds": args.settle_s, "steps": m["settle_steps"]},
         **{k_: round(v, 4) for k_, v in parts.items()},
         **({"split": m["split"]} if m.get("split") else {}),
         **({"launch_timing": m["launch_timing"]} if m.get("launch_timing") else {}),
         **({"halo_batch": m["halo_batch"]} if m.get("halo_batch") else {}),
+        **({"batch": m["batch_trial"]} if m.get("batch_trial") else {}),
         **({"weak": weak} if weak else {}),
     }
+    if state["multi"]:
+        # an N-GPU line must show that RCCL saw N ranks on N distinct devices
+        problems = []
+        if m.get("rccl"):
+            out["rccl"] = m["rccl"]
+            problems += m["rccl"]["problems"]
+        elif args.exchange == "native":
+            problems.append("no RCCL communicator to report (no native shard)")
+        if m.get("exchange_fallback"):
+            problems.append(f"exchange fell back to torch.distributed P2P: {m['exchange_fallback']}")
+        if world != args.gpus:
+            problems.append(f"--gpus {args.gpus} but {world} rank(s) ran")
+        out["valid"] = not problems
+        if problems:
+            out["invalid_reason"] = "; ".join(problems)
     if args.loopback > 1:
         out["rehearsal"] = (f"one GPU: the middle rank's slab of a {args.loopback}-way row split, its two neighbours "
                             f"the rank itself over a one-rank RCCL communicator (vip_shard_create_loopback); value "
@@ -1195,10 +1319,6 @@ def main():
         print(json.dumps(out), flush=True)
     if state["multi"]:
         dist.destroy_process_group()
-    if args.graph:  # two HIP runtimes are loaded (preload_system_rocm): skip their destructors
-        sys.stdout.flush()
-        sys.stderr.flush()
-        os._exit(0)
 
 
 if __name__ == "__main__":

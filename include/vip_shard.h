@@ -54,6 +54,7 @@ extern "C" {
 
 #define VIP_ERR_COMM 10004         /* an RCCL call failed (vip_shard_last_error) */
 #define VIP_ERR_COMM_TIMEOUT 10005 /* communicator set-up not complete before the timeout */
+#define VIP_ERR_UNSUPPORTED 10006  /* not available with the RCCL bound in this process */
 
 #define VIP_SHARD_ID_BYTES 128 /* == NCCL_UNIQUE_ID_BYTES */
 
@@ -147,11 +148,27 @@ int vip_shard_set_frames_launch(vip_shard_t h, int on, int free_cus);
  * always direct (RCCL connects its peers lazily, which a capture cannot do), as is any run
  * on the null stream. A shard's communicator must serve one stream at a time: frames in
  * flight on several streams take one shard each. Up to 64 graphs are kept per shard; a
- * change of split or vip_shard_set_graph(h, 0) drops them. */
+ * change of split or vip_shard_set_graph(h, 0) drops them (waiting on an event the shard
+ * owns, so the caller's streams need not outlive the shard). Turning it on returns
+ * VIP_ERR_UNSUPPORTED when the RCCL bound in the process is older than 2.27.7 (2.26.6, the
+ * copy torch bundles, crashes capturing a send/recv group). If a capture fails, the frame
+ * runs directly (its exchange still happens, so the peers are not left waiting), the
+ * error goes to stderr and graph mode turns itself off for the shard. */
 int vip_shard_set_graph(vip_shard_t h, int on);
 
 /* Number of graphs a shard holds (graph mode). */
 int vip_shard_graph_count(vip_shard_t h, int* count);
+
+/* ncclGetVersion of the RCCL bound in this process (e.g. 22707 for 2.27.7). */
+int vip_shard_rccl_version(int* version);
+
+/* What the shard's RCCL communicator reports about itself (ncclCommCount,
+ * ncclCommUserRank, ncclCommCuDevice): ranks in the communicator, this shard's rank in it,
+ * its HIP device. A loopback shard reports 1 / 0 / the current device. */
+int vip_shard_comm_info(vip_shard_t h, int* count, int* user_rank, int* device);
+
+/* PCI bus id ("dddd:bb:dd.f") of the shard's device (hipDeviceGetPCIBusId); len >= 13. */
+int vip_shard_pci_bus_id(vip_shard_t h, char* bus_id, int len);
 
 /* Test transport, one GPU: shard `rank` of an nranks-way geometry whose row neighbours are
  * the shard ITSELF over a one-rank RCCL communicator. The halo above receives the shard's

@@ -15,6 +15,8 @@
 #   bench=CFG[,A,..]    bench line              -> ${TAG}_CFG_bench.json (A: extra bench.py args)
 #   stats=CFG[,A,..]    rocprofv3 --kernel-trace --stats of a short bench run
 #                                               -> ${TAG}_CFG_kernel_stats.csv, ${TAG}_CFG_busy.json
+#   iso=CFG[,A,..]      rocprofv3 --kernel-trace of a one-stream, one-frame-per-launch bench run: the last
+#                       300 launches of each filter kernel -> ${TAG}_CFG_isolated.csv
 #   pmc=CFG[,A,..]      one rocprofv3 --pmc pass per counter set -> ${TAG}_CFG_pmc.json
 #   rehearse=CFG,N[,A]  the N > 1 native path on one GPU: bench.py --rehearse-native --loopback N A..
 #                                               -> ${TAG}_CFG_loopbackN.json
@@ -28,7 +30,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 O=gpurun_out
 
 fail() { echo "step '$1' failed rc=$2"; [ -n "${3:-}" ] && tail -25 "$3"; exit "$2"; }
@@ -60,17 +62,25 @@ for step in "$@"; do
     stats)
       cfg=${A[0]}; steps=20; [ $cfg = c5 ] && steps=5; d=$O/prof_${TAG}_$cfg
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
-        python bench.py --config $cfg --steps $steps --warmup 3 --no-cpu-baseline "${A[@]:1}" > $d.log 2>&1
+        python bench.py --config $cfg --steps $steps --warmup 3 --no-cpu-baseline --batch 1 "${A[@]:1}" > $d.log 2>&1
       rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
       cp $d/run_kernel_stats.csv $O/${TAG}_${cfg}_kernel_stats.csv
       python scripts/kernel_busy.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_busy.json > /dev/null || fail "$step" $?
       head -4 $O/${TAG}_${cfg}_kernel_stats.csv | cut -c1-200 ;;
+    iso)
+      cfg=${A[0]}; steps=400; [ $cfg = c5 ] && steps=240; [ $cfg = c4 ] && steps=300; d=$O/iso_${TAG}_$cfg
+      timeout -k 10 500 rocprofv3 --kernel-trace -d $d -o run --output-format csv -- \
+        python bench.py --config $cfg --streams 1 --batch 1 --steps $steps --warmup 3 --no-cpu-baseline \
+        "${A[@]:1}" > $d.log 2>&1
+      rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
+      python scripts/isolated_sample.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_isolated.csv --last 300 \
+        || fail "$step" $? ;;
     pmc)
       cfg=${A[0]}; d=$O/pmc_${TAG}_$cfg; mkdir -p $d; i=0
       for set in "${PMC_SETS[@]}"; do
         i=$((i+1))
         timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $set -d $d/p$i -o run --output-format csv -- \
-          python bench.py --config $cfg --streams 1 --steps 5 --warmup 1 --settle-s 0.3 --no-cpu-baseline \
+          python bench.py --config $cfg --streams 1 --batch 1 --steps 5 --warmup 1 --settle-s 0.3 --no-cpu-baseline \
           "${A[@]:1}" > $d/p$i.log 2>&1
         rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || fail "$step pass $i" $rc $d/p$i.log
       done

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Launch durations of a single-stream run from a rocprofv3 kernel trace, for the
+roofline's launch-time evidence (bench.py isolated_sample).
+
+usage: isolated_sample.py <run_kernel_trace.csv> <out.csv> [--last N] [--min-us U]
+
+Keeps, for every kernel whose launches took at least U us (default 5: the filter kernels,
+not torch's buffer fills), its last N launches (default 300: the timed region and what
+follows it, after bench.py's clock settle) that overlap no other launch. Writes one row per
+launch: kernel (exact template signature, as vip_launched_kernels names it), index (its
+position among that kernel's launches), duration_ns. Prints a per-kernel summary."""
+import csv
+import statistics
+import sys
+
+
+def main():
+    args = sys.argv[1:]
+    last = int(args[args.index("--last") + 1]) if "--last" in args else 300
+    min_us = float(args[args.index("--min-us") + 1]) if "--min-us" in args else 5.0
+    rows = list(csv.DictReader(open(args[0])))
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    per = {}
+    end_max = -1
+    for i, (s, e, n) in enumerate(iv):
+        nxt = iv[i + 1][0] if i + 1 < len(iv) else e
+        tol = min(1000, (e - s) // 10)  # back-to-back launches touch by a few hundred ns in the trace
+        alone = s >= end_max - tol and e <= nxt + tol
+        end_max = max(end_max, e)
+        per.setdefault(n, []).append((e - s, alone))
+    with open(args[1], "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["kernel", "index", "duration_ns"])
+        for n, ds in per.items():
+            if statistics.median(d for d, _ in ds) < min_us * 1e3:
+                continue
+            keep = [(i, d) for i, (d, ok) in enumerate(ds) if ok][-last:]
+            for i, d in keep:
+                w.writerow([n, i, d])
+            v = [d for _, d in keep]
+            print(f"{len(v):5d} of {len(ds):6d} launches, mean {sum(v) / len(v) / 1e3:9.2f} us, median "
+                  f"{statistics.median(v) / 1e3:9.2f} us: {n[:110]}")
+
+
+if __name__ == "__main__":
+    main()

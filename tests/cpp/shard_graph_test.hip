@@ -46,13 +46,20 @@ static void on_segv(int sig) {
 int main(int argc, char** argv) {
     signal(SIGSEGV, on_segv);
     signal(SIGABRT, on_segv);
-    int nitr = -1, split = 0;
+    int nitr = -1, split = 0, fail_capture = 0;
     std::vector<std::string> pos;
     for (int i = 1; i < argc; ++i) {
         if (!std::strcmp(argv[i], "--texture") && i + 1 < argc) nitr = std::atoi(argv[++i]);
         else if (!std::strcmp(argv[i], "--split")) split = 1;
+        else if (!std::strcmp(argv[i], "--fail-capture")) fail_capture = 1;
         else pos.push_back(argv[i]);
     }
+    // --fail-capture: every capture fails (the library's test knob); each frame must still run
+    // directly, with its exchange, and graph mode must switch itself off
+    if (fail_capture) setenv("VIP_SHARD_TEST_FAIL_CAPTURE", "1", 1);
+    int rccl = 0;
+    CHECK(vip_shard_rccl_version(&rccl));
+    std::printf("RCCL %d\n", rccl);
     const int width = pos.size() >= 4 ? std::atoi(pos[0].c_str()) : 3840;
     const int own = pos.size() >= 4 ? std::atoi(pos[1].c_str()) : 270;
     const int ksize = pos.size() >= 4 ? std::atoi(pos[2].c_str()) : 15;
@@ -113,6 +120,21 @@ int main(int argc, char** argv) {
     int ng = 0;
     CHECK(vip_shard_graph_count(sh[0], &ng));
     std::printf("graph frames equal the direct frames (%d graphs on shard 0)\n", ng);
+    if (fail_capture) {
+        if (ng != 0) {
+            std::fprintf(stderr, "a failed capture left %d graphs\n", ng);
+            return 1;
+        }
+        std::printf("failed captures fell back to direct frames, graph mode off\n");
+    }
+    // the caller's streams need not outlive the shard: destroy one, then drop the graphs
+    if (!fail_capture && ng > 0) {
+        CHECK(hipDeviceSynchronize());
+        for (int i = 0; i < S; ++i) CHECK(hipStreamDestroy(st[i]));
+        for (int i = 0; i < S; ++i) CHECK(vip_shard_set_graph(sh[i], 0));
+        for (int i = 0; i < S; ++i) CHECK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+        std::printf("graphs dropped after their streams were destroyed\n");
+    }
     // host enqueue and device time per frame, direct vs graph (frames in flight on S streams)
     for (int graph = 0; graph < 2; ++graph) {
         for (int i = 0; i < S; ++i) CHECK(vip_shard_set_graph(sh[i], graph));

@@ -195,50 +195,71 @@ def test_bench_gpus_2_from_a_plain_shell_launches_ranks():
     assert r.returncode not in (0, 124)
 
 
-GRAPH_PROBE = r'''
-import json, os, sys
-graph = "--graph" in sys.argv
-if graph and sys.argv[1] == "crash":
-    sys.exit(7)
-print("rank", os.environ["RANK"], "says hello", flush=True)
-if os.environ["RANK"] == "0":
-    print(json.dumps({"metric": "m", "value": 2.0 if graph else 1.0}), flush=True)
-'''
-
-
-@pytest.mark.parametrize("mode", ["ok", "crash"])
-def test_launch_with_graph_attempt_prints_one_line(tmp_path, mode, capfd):
-    """`python bench.py --gpus N` (native exchange, no --graph/--no-graph): a first run with
-    graph capture; when it fails, the same run without it. Exactly one JSON line either way,
-    saying which run it came from; other stdout lines pass through."""
-    script = tmp_path / "gprobe.py"
-    script.write_text(GRAPH_PROBE)
-    rc = bench.launch_with_graph_attempt(2, [mode], timeout_s=120, script=str(script))
-    out = capfd.readouterr().out
-    lines = [json.loads(x) for x in out.splitlines() if x.startswith("{")]
-    assert rc == 0 and len(lines) == 1
-    assert "says hello" in out
-    if mode == "ok":
-        assert lines[0]["value"] == 2.0 and lines[0]["graph_attempt"].startswith("ok")
-    else:
-        assert lines[0]["value"] == 1.0 and lines[0]["graph_attempt"].startswith("failed (the run with graph")
+def test_default_multi_gpu_run_is_one_plain_launch(monkeypatch):
+    """`python bench.py --gpus N` starts the ranks ONCE with the arguments it was given: no
+    graph-capture attempt, no second HIP runtime or RCCL in a rank."""
+    calls = []
+    monkeypatch.setattr(bench, "launch_ranks", lambda n, argv, timeout_s=0, script=None: calls.append((n, argv)) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and calls == [(8, ["--gpus", "8"])]
+    assert not any("graph" in a for a in calls[0][1])
+    for gone in ("preload_system_rocm", "launch_with_graph_attempt", "SYSTEM_ROCM"):
+        assert not hasattr(bench, gone)
+    with pytest.raises(SystemExit):  # and no --graph option to ask for it
+        monkeypatch.setattr(sys, "argv", ["bench.py", "--graph"])
+        bench.parse()
 
 
 def test_native_trial_forms_keep_buffers_on_one_stream():
-    """The N > 1 native trial's forms (streams S, split, frames per RCCL group B, graph):
+    """The N > 1 native trial's forms (streams S, split, frames per RCCL group B, shared):
     every S of TRIAL_STREAMS appears, each (S, B) keeps buffer i % NBUF on one stream, the
-    texture filter has no split form, and graph forms appear only when asked for."""
-    forms = bench.native_forms(bench.TRIAL_STREAMS, texture=False, graph=False)
+    texture filter has no split form, and --batch restricts B."""
+    forms = bench.native_forms(bench.TRIAL_STREAMS, texture=False)
     assert {f[0] for f in forms} == set(bench.TRIAL_STREAMS)
-    assert all(bench.NBUF % (s * b) == 0 and not g for s, _, b, g, _ in forms)
-    assert {(s, sp) for s, sp, _, _, _ in forms} == {(s, sp) for s in bench.TRIAL_STREAMS for sp in (True, False)}
+    assert all(bench.NBUF % (s * b) == 0 for s, _, b, _ in forms)
+    assert {(s, sp) for s, sp, _, _ in forms} == {(s, sp) for s in bench.TRIAL_STREAMS for sp in (True, False)}
     # shared launches: only after the exchange (no split) and for more than one frame
-    assert all(not sp and b > 1 for _, sp, b, _, sh in forms if sh is not None)
-    assert {(s, b, sh) for s, _, b, _, sh in forms if sh is not None} == {
+    assert all(not sp and b > 1 for _, sp, b, sh in forms if sh is not None)
+    assert {(s, b, sh) for s, _, b, sh in forms if sh is not None} == {
         (s, b, fc) for s in bench.TRIAL_STREAMS for b in bench.halo_batches(s) if b > 1 for fc in bench.SHARED_FREE_CUS}
-    tex = bench.native_forms([2], texture=True, graph=True)
-    assert all(not sp and sh is None for _, sp, _, _, sh in tex) and [f for f in tex if f[3]] == [(2, False, 1, True, None)]
+    tex = bench.native_forms([2], texture=True)
+    assert all(not sp and sh is None for _, sp, _, sh in tex)
     assert len(set(forms)) == len(forms)
+    assert {b for _, _, b, _ in bench.native_forms(bench.TRIAL_STREAMS, texture=False, batches=[3])} == {3}
+
+
+def test_single_gpu_trial_uses_the_multi_gpu_grid():
+    """N = 1 (plain and adaptive) is timed over the same streams x frames-per-launch grid
+    as the N > 1 trial, B = 1 included."""
+    one = bench.single_gpu_forms(bench.TRIAL_STREAMS)
+    assert set(one) == {(s, b) for s, _, b, _ in bench.native_forms(bench.TRIAL_STREAMS, texture=False)}
+    assert (2, 1) in one and (2, 6) in one and (4, 3) in one
+    assert bench.single_gpu_forms([2], [1]) == [(2, 1)]
+
+
+class _FakeShard:
+    def __init__(self, count, user_rank, device, bus):
+        self.i = dict(count=count, user_rank=user_rank, device=device, pci_bus_id=bus)
+
+    def comm_info(self):
+        return dict(self.i)
+
+
+def test_rccl_evidence_flags_what_is_not_an_n_gpu_run(monkeypatch):
+    """The line's `rccl` block: RCCL's own count / user rank / device per rank, and the
+    problems that make a line invalid (a communicator of another size, two ranks on one
+    device, communicators of one rank that disagree)."""
+    import various_image_processings_amd.sharded as sh
+    monkeypatch.setattr(sh, "rccl_version", lambda: 22606)
+    ok = bench.rccl_evidence([_FakeShard(1, 0, 0, "0000:05:00.0")] * 2, 0, 1, 1)
+    assert ok["problems"] == [] and ok["count"] == 1 and ok["distinct_devices"] == 1 and ok["rccl_version"] == 22606
+    bad = bench.rccl_evidence([_FakeShard(1, 0, 0, "0000:05:00.0")], 0, 1, 8)
+    assert bad["problems"] and "expected 8" in bad["problems"][0]
+    mixed = bench.rccl_evidence([_FakeShard(1, 0, 0, "b"), _FakeShard(2, 0, 0, "b")], 0, 1, 1)
+    assert any("disagree" in p for p in mixed["problems"])
 
 
 def test_launched_prefers_the_multi_frame_form():

@@ -336,7 +336,7 @@ def test_loopback_batch(dev, oracle, split, shared, adaptive):
 
 
 @pytest.mark.parametrize("argv", [[], ["--split"], ["1200", "300", "5", "3", "--texture", "5"],
-                                  ["2000", "700", "31", "8"]])
+                                  ["2000", "700", "31", "8"], ["--fail-capture"]])
 def test_loopback_graph_replay_cpp(argv):
     """Graph mode (vip_shard_set_graph) from C++ (tests/cpp/shard_graph_test, outside torch):
     loopback shards, one per stream, two frames in flight; every frame replayed from its
@@ -347,3 +347,43 @@ def test_loopback_graph_replay_cpp(argv):
     assert os.path.exists(exe), "build first"
     r = subprocess.run([exe] + argv, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "graph frames equal the direct frames" in r.stdout, r.stdout + r.stderr[-3000:]
+    if "--fail-capture" in argv:
+        # every capture failed: each frame still ran directly (its exchange included), graph
+        # mode switched itself off, and the library said so
+        assert "fell back to direct frames" in r.stdout and "graph capture failed" in r.stderr
+    else:
+        assert "graphs dropped after their streams were destroyed" in r.stdout
+
+
+def test_comm_info_one_rank_and_loopback(dev):
+    """vip_shard_comm_info: RCCL's own count / user rank / device of a shard's communicator.
+    A one-rank shard and a loopback shard (one-rank communicator, itself as neighbours) both
+    report 1 / 0 / the current device, and the device's PCI bus id."""
+    torch = dev.torch_
+    cur = torch.cuda.current_device()
+    for s in (NativeShard(900, 500, 15, 0, 1, native_unique_id()), NativeShard(900, 4 * 200, 15, 2, 4, None,
+                                                                             loopback=True)):
+        info = s.comm_info()
+        assert (info["count"], info["user_rank"], info["device"]) == (1, 0, cur), info
+        bus = info["pci_bus_id"]
+        assert len(bus.split(":")) == 3 and "." in bus, bus
+        s.close()
+
+
+def test_graph_mode_refused_below_the_verified_rccl(dev):
+    """vip_shard_set_graph refuses graph mode (VIP_ERR_UNSUPPORTED) when the RCCL bound in
+    this process is older than 2.27.7 -- in a torch process that is torch's bundled copy,
+    whose capture of a send/recv group crashes -- and accepts it otherwise."""
+    from various_image_processings_amd.sharded import rccl_version
+    v = rccl_version()
+    assert v > 20000, v
+    s = NativeShard(900, 4 * 200, 15, 2, 4, None, loopback=True)
+    if v < S.GRAPH_MIN_RCCL_VERSION:
+        with pytest.raises(S.ShardError) as e:
+            s.set_graph(True)
+        assert e.value.code == S.VIP_ERR_UNSUPPORTED and "2.27.7" in str(e.value)
+        assert s.graph_count() == 0
+    else:
+        s.set_graph(True)
+    s.set_graph(False)  # turning it off is always allowed
+    s.close()

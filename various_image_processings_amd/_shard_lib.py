@@ -13,6 +13,8 @@ LIB_PATH = os.path.join(_lib._HERE, "libvip_shard.so")
 
 VIP_ERR_COMM = 10004
 VIP_ERR_COMM_TIMEOUT = 10005
+VIP_ERR_UNSUPPORTED = 10006
+GRAPH_MIN_RCCL_VERSION = 22707  # vip_shard_set_graph needs RCCL >= 2.27.7
 VIP_SHARD_ID_BYTES = 128
 VIP_SHARD_RCCL = 0
 VIP_SHARD_LOCAL = 1
@@ -38,6 +40,9 @@ SIGNATURES = {
     "vip_shard_set_graph": (_i, [_p, _i]),
     "vip_shard_set_frames_launch": (_i, [_p, _i, _i]),
     "vip_shard_graph_count": (_i, [_p, _ip]),
+    "vip_shard_rccl_version": (_i, [_ip]),
+    "vip_shard_comm_info": (_i, [_p, _ip, _ip, _ip]),
+    "vip_shard_pci_bus_id": (_i, [_p, ctypes.c_char_p, _i]),
     "vip_shard_create_loopback": (_i, [_pp, _i, _i, _i, _i, _f, _f, _i, _i, _i, _i, _i]),
     "vip_shard_last_error": (ctypes.c_char_p, []),
     "vip_shard_destroy": (_i, [_p]),
@@ -50,10 +55,10 @@ _lib_shard = None
 class ShardError(_lib.VipError):
     def __init__(self, func: str, code: int):
         self.code = code
-        if code in (VIP_ERR_COMM, VIP_ERR_COMM_TIMEOUT):
+        if code in (VIP_ERR_COMM, VIP_ERR_COMM_TIMEOUT, VIP_ERR_UNSUPPORTED):
             detail = lib().vip_shard_last_error().decode(errors="replace")
-            RuntimeError.__init__(self, f"{func} failed with status {code}: "
-                                        f"{'RCCL error' if code == VIP_ERR_COMM else 'timeout'}: {detail}")
+            what = {VIP_ERR_COMM: "RCCL error", VIP_ERR_COMM_TIMEOUT: "timeout"}.get(code, "unsupported")
+            RuntimeError.__init__(self, f"{func} failed with status {code}: {what}: {detail}")
         else:
             super().__init__(func, code)
 

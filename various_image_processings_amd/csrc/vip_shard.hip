@@ -123,6 +123,7 @@ struct vip_shard_s {
         size_t pitch;
         hipStream_t stream;
         hipGraphExec_t exec;
+        hipEvent_t done;  // shard-owned, recorded after every replay: freed without the caller's stream
     };
     int graph = 0;
     bool warm = false;           // one direct exchange done: RCCL connects peers lazily, a capture cannot
@@ -326,12 +327,30 @@ struct DeviceGuard {  // restores the caller's current device
     }
 };
 
-void free_graphs(vip_shard_s* h) {
-    for (auto& g : h->graphs) {
-        (void)hipStreamSynchronize(g.stream);  // a replay may still be in flight
-        (void)hipGraphExecDestroy(g.exec);
+// A replay may still be in flight: wait on the shard's own event for it, never on the
+// caller's stream (which vip_shard.h does not require to outlive the shard).
+void free_graph(vip_shard_s::Graph& g) {
+    if (g.done) {
+        (void)hipEventSynchronize(g.done);
+        (void)hipEventDestroy(g.done);
     }
+    (void)hipGraphExecDestroy(g.exec);
+}
+
+void free_graphs(vip_shard_s* h) {
+    for (auto& g : h->graphs) free_graph(g);
     h->graphs.clear();
+}
+
+// RCCL builds whose capture of a ncclSend/ncclRecv group was verified: 2.27.7 (the image's
+// /opt/rocm/lib/librccl.so; tests/cpp/shard_graph_test). torch's bundled 2.26.6 crashes
+// on the first capture in every capture mode (profiles/r04_graph_capture.txt), and inside a
+// torch process this library's RCCL symbols bind to that copy.
+constexpr int kGraphMinRcclVersion = 22707;
+
+int rccl_version() {
+    int v = 0;
+    return ncclGetVersion(&v) == ncclSuccess ? v : 0;
 }
 
 constexpr size_t kMaxGraphs = 64;  // captured (slab, out, stream) combinations kept per shard
@@ -535,6 +554,11 @@ int vip_shard_set_frames_launch(vip_shard_t h, int on, int free_cus) {
 int vip_shard_set_graph(vip_shard_t h, int on) {
     if (!h || (on != 0 && on != 1)) return VIP_ERR_INVALID_ARGUMENT;
     if (h->transport != VIP_SHARD_RCCL) return VIP_ERR_INVALID_ARGUMENT;
+    if (on && rccl_version() < kGraphMinRcclVersion) {
+        g_last_error = "graph mode needs RCCL >= 2.27.7 (the RCCL bound in this process is " +
+                       std::to_string(rccl_version()) + "; older builds crash capturing a send/recv group)";
+        return VIP_ERR_UNSUPPORTED;
+    }
     if (!on) {
         DeviceGuard guard;
         (void)hipSetDevice(h->device);
@@ -542,6 +566,27 @@ int vip_shard_set_graph(vip_shard_t h, int on) {
     }
     h->graph = on;
     return 0;
+}
+
+int vip_shard_rccl_version(int* version) {
+    if (!version) return VIP_ERR_INVALID_ARGUMENT;
+    *version = rccl_version();
+    return 0;
+}
+
+int vip_shard_comm_info(vip_shard_t h, int* count, int* user_rank, int* device) {
+    if (!h || !count || !user_rank || !device || h->transport != VIP_SHARD_RCCL || !h->nccl)
+        return VIP_ERR_INVALID_ARGUMENT;
+    ncclResult_t e = ncclCommCount(h->nccl, count);
+    if (e != ncclSuccess) return comm_fail(e, "ncclCommCount");
+    if ((e = ncclCommUserRank(h->nccl, user_rank)) != ncclSuccess) return comm_fail(e, "ncclCommUserRank");
+    if ((e = ncclCommCuDevice(h->nccl, device)) != ncclSuccess) return comm_fail(e, "ncclCommCuDevice");
+    return 0;
+}
+
+int vip_shard_pci_bus_id(vip_shard_t h, char* bus_id, int len) {
+    if (!h || !bus_id || len < 13) return VIP_ERR_INVALID_ARGUMENT;  // "0000:00:00.0" + NUL
+    return (int)hipDeviceGetPCIBusId(bus_id, len, h->device);
 }
 
 int vip_shard_graph_count(vip_shard_t h, int* count) {
@@ -644,11 +689,12 @@ int vip_shard_run_batch(vip_shard_t h, int n, uint8_t* const* d_slabs, uint8_t* 
 // communicator's kernels concurrently.
 static int run_graph(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitch, hipStream_t s) {
     for (const auto& g : h->graphs)
-        if (g.slab == slab && g.out == out && g.pitch == out_pitch && g.stream == s)
-            return (int)hipGraphLaunch(g.exec, s);
-    if (h->graphs.size() >= kMaxGraphs) {
-        VIP_HIP_TRY(hipStreamSynchronize(h->graphs.front().stream));  // the oldest graph may still be in flight
-        (void)hipGraphExecDestroy(h->graphs.front().exec);
+        if (g.slab == slab && g.out == out && g.pitch == out_pitch && g.stream == s) {
+            VIP_HIP_TRY(hipGraphLaunch(g.exec, s));
+            return (int)hipEventRecord(g.done, s);
+        }
+    if (h->graphs.size() >= kMaxGraphs) {  // the oldest graph may still be in flight: free_graph waits
+        free_graph(h->graphs.front());
         h->graphs.erase(h->graphs.begin());
     }
     // nothing is enqueued yet: if the stream cannot capture, run this frame directly
@@ -659,16 +705,34 @@ static int run_graph(vip_shard_t h, uint8_t* slab, uint8_t* out, size_t out_pitc
     const int rc = enqueue_run(h, slab, out, out_pitch, s, nullptr);
     hipGraph_t graph = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &graph);
-    if (rc || e != hipSuccess) {
-        if (graph) (void)hipGraphDestroy(graph);
-        return rc ? rc : (int)e;
-    }
     hipGraphExec_t exec = nullptr;
-    const hipError_t ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) return (int)ei;
-    h->graphs.push_back({slab, out, out_pitch, s, exec});
-    return (int)hipGraphLaunch(exec, s);
+    hipError_t ei = hipErrorUnknown;
+    // VIP_SHARD_TEST_FAIL_CAPTURE=1: treat every capture as failed (the recovery path's test,
+    // tests/cpp/shard_graph_test --fail-capture)
+    static const bool fail_capture = [] {
+        const char* v = std::getenv("VIP_SHARD_TEST_FAIL_CAPTURE");
+        return v && v[0] == '1';
+    }();
+    if (!rc && e == hipSuccess && !fail_capture) ei = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    hipEvent_t done = nullptr;
+    if (ei == hipSuccess) ei = hipEventCreateWithFlags(&done, hipEventDisableTiming);
+    if (ei != hipSuccess) {
+        // The capture failed, so this rank's sends and receives for the frame never ran,
+        // while the peers ran (or replay) their half of the exchange: run the frame directly
+        // now so every rank still performs it, and leave graph mode for this shard (a
+        // second capture would fail the same way).
+        if (exec) (void)hipGraphExecDestroy(exec);
+        (void)hipGetLastError();
+        fprintf(stderr, "vip_shard: graph capture failed (run %d, end capture %d, instantiate %d): graph mode off, "
+                        "running the frame directly\n", rc, (int)e, (int)ei);
+        h->graph = 0;
+        free_graphs(h);
+        return enqueue_run(h, slab, out, out_pitch, s, nullptr);
+    }
+    h->graphs.push_back({slab, out, out_pitch, s, exec, done});
+    VIP_HIP_TRY(hipGraphLaunch(exec, s));
+    return (int)hipEventRecord(done, s);
 }
 
 int vip_shard_run(vip_shard_t h, uint8_t* d_slab, uint8_t* d_out, size_t out_pitch, void* stream) {

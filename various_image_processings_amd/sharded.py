@@ -226,6 +226,28 @@ class ShardedBilateral:
                     _lib.check(name, rc)
         return run
 
+    def batch_launcher(self, free_cus: int = 0):
+        """A lean callable f(src_ptrs, dst_ptrs, hip_stream): the whole own-row range of
+        several frames in shared launches (vip_bilateral_run_rows_batch /
+        vip_adaptive_run_rows_batch, up to 6 frames per launch), no exchange. Raw device
+        addresses, unchecked."""
+        import ctypes
+        from . import _lib
+        g = self.geo
+        lo, hi = self._clamp
+        p = g.width * 3
+        name = "vip_adaptive_run_rows_batch" if self.adaptive else "vip_bilateral_run_rows_batch"
+        fn = getattr(_lib.lib(), name)
+        h = self.impl._h
+
+        def run(srcs, dsts, stream):
+            n = len(srcs)
+            rc = fn(h, n, (ctypes.c_void_p * n)(*srcs), p, (ctypes.c_void_p * n)(*dsts), p, g.own, g.radius, lo, hi,
+                    int(free_cus), stream)
+            if rc:
+                _lib.check(name, rc)
+        return run
+
 
 def texture_halo_rows(ksize: int) -> int:
     """Rows one texture iteration reaches beyond its output rows: the JBF radius
@@ -307,6 +329,15 @@ def native_rows(frame_height: int, world: int, rank: int) -> tuple[int, int]:
     return b.value, b.value + n.value
 
 
+def rccl_version() -> int:
+    """ncclGetVersion of the RCCL bound in this process (vip_shard_rccl_version)."""
+    import ctypes
+    from . import _shard_lib as S
+    v = ctypes.c_int()
+    S.call("vip_shard_rccl_version", ctypes.byref(v))
+    return v.value
+
+
 def _native_halo(ksize: int, nitr) -> int:
     """Halo rows of a native shard: r = ksize / 2, or nitr texture iterations deep."""
     return ksize // 2 if nitr is None else nitr * texture_halo_rows(ksize)
@@ -347,9 +378,23 @@ class NativeShard:
         S.call("vip_shard_set_split", self._h, 1 if split else 0)
 
     def set_graph(self, on: bool) -> None:
-        """vip_shard_set_graph: replay one captured hipGraph per (slab, out, stream)."""
+        """vip_shard_set_graph: replay one captured hipGraph per (slab, out, stream). Raises
+        ShardError (VIP_ERR_UNSUPPORTED) when the RCCL bound in this process is older than
+        2.27.7 -- inside a torch process that is torch's bundled 2.26.6, so graph mode is a
+        C/C++ feature (tests/cpp/shard_graph_test)."""
         from . import _shard_lib as S
         S.call("vip_shard_set_graph", self._h, 1 if on else 0)
+
+    def comm_info(self) -> dict:
+        """What RCCL reports about this shard's communicator (vip_shard_comm_info:
+        ncclCommCount, ncclCommUserRank, ncclCommCuDevice) and the device's PCI bus id."""
+        import ctypes
+        from . import _shard_lib as S
+        c, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        S.call("vip_shard_comm_info", self._h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(d))
+        bus = ctypes.create_string_buffer(32)
+        S.call("vip_shard_pci_bus_id", self._h, bus, 32)
+        return dict(count=c.value, user_rank=r.value, device=d.value, pci_bus_id=bus.value.decode())
 
     def set_frames_launch(self, on: bool, free_cus: int = 0) -> None:
         """vip_shard_set_frames_launch: a batch's frames share filter launches that leave
