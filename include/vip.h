@@ -157,7 +157,9 @@ int vip_bilateral_set_wide(int mode);
  * distinct streams among its last 8 plain-bilateral launches (at most 4), so frames in
  * flight on several streams each get a tiling sized for their share of the CUs; 1..4 forces
  * the count (a measurement knob: e.g. timing one frame alone with the tiling the in-flight
- * frames use). Results are identical for every setting. */
+ * frames use). The count is of streams, not of launches outstanding: a caller that
+ * alternates streams but waits for each frame counts 2 or more too, and should force 1.
+ * Results are identical for every setting. */
 int vip_bilateral_set_frames_in_flight(int n);
 
 /* ---- adaptive bilateral: CudaAdaptiveBilateralFilter

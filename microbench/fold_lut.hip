@@ -1,0 +1,150 @@
+// Microbenchmark for VERDICT r04 item 7: fold the spatial weight of the plain C2 bilateral
+// (r = 7, sigma_color 30) into the colour LUT, one table per squared tap distance.
+//
+// Today's tap (vip_bilateral.hip, 32 interleaved LUT copies, lane l reads copy l mod 32):
+//   v_sad_u8 -> v_lshl_or (d * 128 + 4 * lane) -> ds_read_b32 wc -> v_mul (ws * wc, ws an
+//   SGPR) -> 3 v_fma -> v_add                                  7 VALU + 1 LDS, conflict free
+// Folded tap: RN(ws(r^2) * wc[d]) in one table per r^2 class (24 classes at r = 7, d = 0..431
+// plus one zero: 41.5 KB per copy, so ONE copy fits beside the tile plane -- the 32-copy
+// layout would need 1.3 MB), addressed by a saturating v_mad_legacy_u16 (min(4d + B0, 65535),
+// the class table's base in the ds_read immediate):
+//   v_sad_u8 -> v_mad_legacy_u16 clamp -> ds_read_b32 w -> 3 v_fma -> v_add
+//                                                        6 VALU + 1 LDS, lanes spread over
+//                                                        the 32 banks by their data
+// Both kinds run the same data: 8 outputs per thread, each tap's neighbour a different word
+// of 8 per-lane words of uniform-random RGB (the bench's input statistics), so d has the
+// distribution of |dB| + |dG| + |dR| of uniform bytes. 16 waves per CU, 64 KiB of LUT per
+// workgroup, one workgroup per CU (as C2). Prints ns per wave-tap per SIMD; run it under
+// rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU for the LDS cost.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <vector>
+
+#define ITERS 384
+constexpr int kTaps = 24;    // taps per unrolled block (lcm of the 8 neighbour words and 24 classes);
+                             // ITERS blocks = 64 passes over 144 taps (149 in-disc taps at r = 7)
+constexpr int kClasses = 24;  // distinct r^2 in the r = 7 disc
+constexpr int kDz = 432;      // sigma_color 30: the colour LUT is zero from d = 432
+constexpr int kLutWords = 16384;  // today's 32-copy table region: 64 KiB
+// folded: B0 = 65535 - 4 kDz (odd, like SatLut's), tables from byte T = round_up(B0, 16), entry
+// (class k, d) at T + 4 (k (kDz + 1) + d): address min(4d + B0, 65535) + (T - B0 + 4 k (kDz + 1))
+constexpr int kB0 = 65535 - 4 * kDz;
+constexpr int kT = (kB0 + 15) / 16 * 16;
+constexpr int kLdsBytes = kT + 4 * kClasses * (kDz + 1);
+
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;  // an LDS byte address as a pointer
+__device__ __forceinline__ float lds_f32(uint32_t byte_addr) {
+    return __uint_as_float(*(lds_u32*)(uintptr_t)byte_addr);
+}
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+
+// KIND 0: today's 32-copy LUT + spatial multiply; KIND 1: folded one-copy tables
+template <int KIND>
+__global__ __launch_bounds__(1024) void taps(float* out, const float* __restrict__ lut_src,
+                                             const float* __restrict__ ws) {
+    extern __shared__ uint32_t lut[];
+    for (int i = threadIdx.x; i < kLdsBytes / 4; i += 1024) lut[i] = __float_as_uint(lut_src[i % kLutWords]);
+    __syncthreads();
+    float wsr[kClasses];
+#pragma unroll
+    for (int k = 0; k < kClasses; ++k) wsr[k] = ws[k];
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t w[8], c[8];
+    const uint32_t seed = (blockIdx.x * 1024 + threadIdx.x) * 977u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        w[i] = hash32(seed + i) % 255u | (hash32(seed ^ (i * 31 + 7)) % 255u) << 8 | (hash32(seed * 3 + i) % 255u) << 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        c[i] = hash32(seed + 100 + i) % 255u | (hash32(seed + 200 + i) % 255u) << 8 | (hash32(seed + 300 + i) % 255u) << 16;
+    float pf[8][3];  // the neighbour words as floats, shared by the outputs that meet them
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        for (int ch = 0; ch < 3; ++ch) pf[i][ch] = (float)((w[i] >> (8 * ch)) & 255u);
+    float s0[8], s1[8], s2[8], sk[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s0[i] = s1[i] = s2[i] = sk[i] = 0.f;
+    const uint32_t lane4 = (lane & 31) << 2;
+    const uint32_t b0 = kB0;
+    for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+            const int k = t % kClasses;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const uint32_t nb = w[(t + i) & 7];
+                uint32_t d, ad;
+                asm volatile("v_sad_u8 %0, %1, %2, 0" : "=v"(d) : "v"(nb), "v"(c[i]));
+                float wt;
+                if constexpr (KIND == 0) {
+                    asm volatile("v_lshl_or_b32 %0, %1, 7, %2" : "=v"(ad) : "v"(d), "v"(lane4));
+                    const float wc = lds_f32(ad);  // the table sits at LDS byte 0
+                    wt = wc * wsr[k];  // ws: uniform (an SGPR)
+                } else {
+                    asm volatile("v_mad_legacy_u16 %0, %1, 4, %2 clamp" : "=v"(ad) : "v"(d), "v"(b0));
+                    // the class table's base: T - B0 + 4 k (kDz + 1), a compile-time immediate
+                    wt = lds_f32(ad + (kT - kB0) + 4 * k * (kDz + 1));
+                }
+                const float* p = pf[(t + i) & 7];
+                s0[i] = __builtin_fmaf(p[0], wt, s0[i]);
+                s1[i] = __builtin_fmaf(p[1], wt, s1[i]);
+                s2[i] = __builtin_fmaf(p[2], wt, s2[i]);
+                sk[i] += wt;
+            }
+        }
+    }
+    float s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += s0[i] + s1[i] + s2[i] + sk[i];
+    out[blockIdx.x * 1024 + threadIdx.x] = s;
+}
+
+template <int KIND>
+double run(const char* name, float* d_out, const float* d_lut, const float* d_ws) {
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    const int blocks = 256;
+    hipFuncSetAttribute(reinterpret_cast<const void*>(taps<KIND>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        kLdsBytes);
+    for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(taps<KIND>, dim3(blocks), dim3(1024), kLdsBytes, 0, d_out, d_lut, d_ws);
+    hipEventRecord(e0);
+    const int reps = 5;
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(taps<KIND>, dim3(blocks), dim3(1024), kLdsBytes, 0, d_out, d_lut, d_ws);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms;
+    hipEventElapsedTime(&ms, e0, e1);
+    // wave-taps per SIMD: blocks * 16 waves * ITERS * kTaps * 8 outputs / 1024 SIMDs
+    const double wave_taps = (double)blocks * 16 * ITERS * kTaps * 8 / 1024.0;
+    const double ns = ms / reps * 1e6 / wave_taps;
+    printf("%-52s %8.3f ms per launch  %.3f ns per wave-tap per SIMD\n", name, ms / reps, ns);
+    return ns;
+}
+
+int main() {
+    // today's layout reads words d * 32 + lane (d < 512) of the first 64 KiB; the folded one its
+    // tables above byte kT. Values: the sigma_color 30 LUT (repeated; timing only).
+    std::vector<float> lut(kLutWords), ws(kClasses);
+    for (int i = 0; i < kLutWords; ++i) lut[i] = std::exp(-(float)((i / 32) % 768) * ((i / 32) % 768) / 1800.f);
+    for (int k = 0; k < kClasses; ++k) ws[k] = std::exp(-(float)k / 200.f);
+    float *d_out, *d_lut, *d_ws;
+    hipMalloc(&d_out, 256 * 1024 * sizeof(float));
+    hipMalloc(&d_lut, lut.size() * sizeof(float));
+    hipMalloc(&d_ws, ws.size() * sizeof(float));
+    hipMemcpy(d_lut, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice);
+    hipMemcpy(d_ws, ws.data(), ws.size() * sizeof(float), hipMemcpyHostToDevice);
+    const double a = run<0>("today: 32-copy LUT, sad lshl_or ds_read mul 3fma add", d_out, d_lut, d_ws);
+    const double b = run<1>("folded: 1-copy class tables, sad mad_u16 ds_read 3fma add", d_out, d_lut, d_ws);
+    const double a2 = run<0>("today again", d_out, d_lut, d_ws);
+    printf("folded / today: %.3f\n", b / (0.5 * (a + a2)));
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}

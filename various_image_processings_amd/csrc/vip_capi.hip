@@ -170,9 +170,14 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
 
 // Frames in flight on the current device, for the plain bilateral kernel's small-frame
 // tiling: the distinct streams among the device's last 8 plain-bilateral launches, at most
-// 4 (the hardware queues a process gets by default, GPU_MAX_HW_QUEUES). One stream (or
-// launches that alternate streams one at a time) counts 1. The choice changes the tiling
-// only, never the bytes.
+// 4 (the hardware queues a process gets by default, GPU_MAX_HW_QUEUES). One stream counts
+// 1. The count is of streams, not of launches outstanding: a caller that alternates two
+// streams but waits for each frame before the next also counts 2 (and gets the throughput
+// tiling, e.g. C1's 14.5 instead of 10.7 us for a lone 512 x 512 frame), and after a change
+// of streams the ring keeps the old count for up to 8 launches. Such a caller fixes the
+// count with vip_bilateral_set_frames_in_flight(1). (Checking each recorded stream with
+// hipStreamQuery would cost host time per launch and could touch a destroyed stream.) The
+// choice changes the tiling only, never the bytes.
 static std::atomic<int> g_bil_inflight{0};  // vip_bilateral_set_frames_in_flight: 0 = counted
 static int frames_in_flight(hipStream_t s) {
     constexpr int kDevs = 16, kRing = 8;
