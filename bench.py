@@ -150,6 +150,8 @@ TRIAL_STREAMS = (2, 3, 4)
 # frames per group: 0 free 0.0335, 16 free 0.0268 ms per step, against 0.0311 one launch per
 # frame (profiles/r04_shared_launch.txt).
 SHARED_FREE_CUS = (0, 8, 16, 24, 32)
+# N = 1 trial: a form other than the default must be faster by more than this fraction
+TRIAL_MARGIN = 0.005
 
 
 def native_forms(stream_counts, texture: bool, batches=None) -> list:
@@ -924,8 +926,9 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # fastest.
         trial = {}
         n_trial = 6 * max(8, args.steps // 24)
-        forms = [f for f in cfg.get("single_gpu_forms", single_gpu_forms(s_forms, batches))
-                 if f[0] <= len(streams) and (batches is None or f[1] in batches)] or single_gpu_forms(s_forms, batches)
+        s_first = sorted(s_forms, key=lambda n: n != S)  # the config's stream count first
+        forms = [f for f in cfg.get("single_gpu_forms", single_gpu_forms(s_first, batches))
+                 if f[0] <= len(streams) and (batches is None or f[1] in batches)] or single_gpu_forms(s_first, batches)
         if not forms:
             raise SystemExit(f"bench.py: --batch {args.batch} fits none of the stream counts {s_forms}")
         for n_s, b in forms:
@@ -943,9 +946,17 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             torch.cuda.synchronize(dev)
             trial[(n_s, b)] = (time.perf_counter() - t0) / n_trial * 1e3
         best_s, best_b = min(trial, key=trial.get)
+        # trial noise is ~0.3 % at C2 (r05 lines: s2_batch1 0.1679 against s2_batch2 0.1678 ms):
+        # another form replaces the default (the first form: one frame per launch on the
+        # config's streams, whose kernel the committed PMC and launch samples hold) only when
+        # it is faster by more than TRIAL_MARGIN
+        default = forms[0]
+        if trial[(best_s, best_b)] * (1 + TRIAL_MARGIN) >= trial[default]:
+            best_s, best_b = default
         hb["B"], hb["S"] = best_b, best_s
         res["streams"] = best_s
-        res["batch"] = dict(chosen=best_b, trial_steps=n_trial,
+        res["batch"] = dict(chosen=best_b, streams=best_s, default=f"s{default[0]}_batch{default[1]}",
+                            margin=TRIAL_MARGIN, trial_steps=n_trial,
                             trial_ms_per_step={f"s{s_}_batch{b_}": round(v, 4) for (s_, b_), v in trial.items()})
     res["settle_steps"] = i_settle
     S_run = hb["S"]  # streams the timed steps use
