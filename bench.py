@@ -278,6 +278,11 @@ def parse():
     # frames per shared launch (N = 1) / per RCCL group (N > 1): fixes B in the trial
     # (default: the trial picks from halo_batches(S))
     p.add_argument("--batch", type=int, default=None, choices=[1, 2, 3, 4, 6])
+    # the plain bilateral kernel's small-frame tiling plans for this many frames in flight
+    # (vip_bilateral_set_frames_in_flight) instead of counting the streams in use: a
+    # one-stream profiling run of a small frame then launches the instantiation a multi-
+    # stream line timed (scripts/gpu.sh iso / pmc)
+    p.add_argument("--frames-in-flight", type=int, default=0, choices=[0, 1, 2, 3, 4])
     # --gpus N > 1 without WORLD_SIZE in the environment: this process starts the N ranks
     # itself (a child torchrun) and ends them after this many seconds
     p.add_argument("--launch-timeout", type=float, default=LAUNCH_TIMEOUT_S)
@@ -926,7 +931,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # fastest.
         trial = {}
         n_trial = 6 * max(8, args.steps // 24)
-        s_first = sorted(s_forms, key=lambda n: n != S)  # the config's stream count first
+        s_first = sorted(s_forms, key=lambda n: n != args.streams)  # the config's stream count first
         forms = [f for f in cfg.get("single_gpu_forms", single_gpu_forms(s_first, batches))
                  if f[0] <= len(streams) and (batches is None or f[1] in batches)] or single_gpu_forms(s_first, batches)
         if not forms:
@@ -1165,6 +1170,8 @@ def main():
 
     import various_image_processings_amd as vip  # noqa: F401  (loads libvip_hip.so or raises)
 
+    if args.frames_in_flight:
+        vip.set_bilateral_frames_in_flight(args.frames_in_flight)
     fixed_streams = args.streams or cfg.get("streams")
     S = args.streams = fixed_streams or 2
     if "tiling" in cfg and world == 1:  # the config's tile shape (include/vip.h tuning knobs)

@@ -8,10 +8,17 @@ Keeps, for every kernel whose launches took at least U us (default 5: the filter
 not torch's buffer fills), its last N launches (default 300: the timed region and what
 follows it, after bench.py's clock settle) that overlap no other launch. Writes one row per
 launch: kernel (exact template signature, as vip_launched_kernels names it), index (its
-position among that kernel's launches), duration_ns. Prints a per-kernel summary."""
+position among that kernel's launches), duration_ns. The trace's argument list is cut off the
+name, which then reads as vip_launched_kernels and the PMC summaries name the kernel.
+Prints a per-kernel summary."""
 import csv
 import statistics
 import sys
+
+
+def strip_args(name: str) -> str:
+    """'void vip::k<7, 16>(vip::StencilArgs)' -> 'void vip::k<7, 16>'"""
+    return name[:name.rfind("(")] if name.endswith(")") else name
 
 
 def main():
@@ -19,7 +26,7 @@ def main():
     last = int(args[args.index("--last") + 1]) if "--last" in args else 300
     min_us = float(args[args.index("--min-us") + 1]) if "--min-us" in args else 5.0
     rows = list(csv.DictReader(open(args[0])))
-    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), strip_args(r["Kernel_Name"])) for r in rows)
     per = {}
     end_max = -1
     for i, (s, e, n) in enumerate(iv):

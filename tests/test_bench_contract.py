@@ -271,3 +271,50 @@ def test_launched_prefers_the_multi_frame_form():
     assert bench.launched([one], "void vip::bilateral_kernel<7,") == one
     assert bench.launched(["void vip::adaptive_kernel<7, 16, true, 4, 512, true>"],
                           "void vip::bilateral_kernel<7,") is None
+
+
+ISO_KERNELS = {"c2": ["void vip::bilateral_kernel<7, 16, false, true, 32, 8, 768, false, 16, false>"],
+               "c3": ["void vip::adaptive_kernel<7, 16, true, 4, 512, true>"],
+               "c4": ["void vip::bilateral_kernel<4, 16, true, true, 32, 8, 32, true, 16, true>"]}
+
+
+@pytest.mark.parametrize("cfg", sorted(ISO_KERNELS))
+def test_isolated_launch_samples_are_large_enough(cfg):
+    """the launch duration behind each headline roofline rests on a
+    committed single-stream rocprofv3 sample (profiles/r05_<cfg>_isolated.csv, via
+    scripts/isolated_sample.py) of at least 200 launches of the exact instantiation, and the
+    committed line's live event-timed launch agrees with it to 3 %."""
+    for kern in ISO_KERNELS[cfg]:
+        s = bench.isolated_sample(cfg, kern)
+        assert s is not None and s["launches"] >= 200, (cfg, kern, s)
+        assert s["min_us"] <= s["median_us"] <= s["max_us"]
+    line = json.loads(open(os.path.join(ROOT, "profiles", f"r05_{cfg}_bench.json")).read().strip().splitlines()[-1])
+    r = line["roofline"]
+    if cfg == "c4":  # the JBF launch (the guide stage's instantiation carries its argument list)
+        launch_ms = [k["avg_launch_ms"] for k in (r["dominant"], r["other"]) if "joint" in k["kernel"]][0]
+    else:
+        launch_ms = r["avg_launch_ms"]
+    iso = bench.isolated_sample(cfg, ISO_KERNELS[cfg][0])["mean_us"] / 1e3
+    assert abs(iso - launch_ms) / launch_ms < 0.03, (cfg, iso, launch_ms)
+    # a guide-stage sample exists too (its name carries the argument list in the trace)
+    if cfg == "c4":
+        import csv
+        rows = list(csv.DictReader(open(os.path.join(ROOT, "profiles", "r05_c4_isolated.csv"))))
+        assert sum(1 for x in rows if x["kernel"].startswith("void vip::texture_guide_fused_kernel<2, false>")) >= 200
+
+
+def test_isolated_sample_script(tmp_path):
+    """scripts/isolated_sample.py keeps the last N non-overlapping launches per kernel above
+    the duration floor."""
+    import subprocess
+    rows = [("k", i * 100, i * 100 + 50) for i in range(10)] + [("j", 2000, 2001), ("k", 2010, 2100), ("k", 2050, 2150)]
+    f = tmp_path / "t.csv"
+    f.write_text("Kernel_Name,Start_Timestamp,End_Timestamp\n" + "".join(f"{n},{s},{e}\n" for n, s, e in rows))
+    out = tmp_path / "o.csv"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "isolated_sample.py"), str(f), str(out), "--last", "4",
+                    "--min-us", "0.01"], check=True, capture_output=True)
+    import csv
+    got = list(csv.DictReader(open(out)))
+    assert [int(r["index"]) for r in got if r["kernel"] == "k"] == [6, 7, 8, 9]  # overlapping pair dropped
+    assert all(int(r["duration_ns"]) == 50 for r in got if r["kernel"] == "k")
+    assert not [r for r in got if r["kernel"] == "j"]  # below the floor
