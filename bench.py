@@ -1254,6 +1254,8 @@ def main():
             if fpl > 1:
                 roof["frames_per_launch"] = fpl
             roof["isolated_sample"] = isolated_sample(args.config, kname)
+            if roof["isolated_sample"] and fpl > 1:  # the sample's launches carry fpl frames each
+                roof["isolated_sample"]["mean_us_per_frame"] = round(roof["isolated_sample"]["mean_us"] / fpl, 2)
             if m["frames_in_flight"] > 1:  # the chip's rate with frames in flight (launches overlap)
                 fl = flops / (ms_per_step * 1e-3) / 1e12
                 roof["in_flight"] = dict(achieved=round(fl, 3), frac=round(fl / PEAK_FP32_TFLOPS, 4), unit="TFLOP/s",

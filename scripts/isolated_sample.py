@@ -2,10 +2,10 @@
 """Launch durations of a single-stream run from a rocprofv3 kernel trace, for the
 roofline's launch-time evidence (bench.py isolated_sample).
 
-usage: isolated_sample.py <run_kernel_trace.csv> <out.csv> [--last N] [--min-us U]
+usage: isolated_sample.py <run_kernel_trace.csv> <out.csv> [--last N] [--min-us U] [--prefix P] [--prefix P]
 
-Keeps, for every kernel whose launches took at least U us (default 5: the filter kernels,
-not torch's buffer fills), its last N launches (default 300: the timed region and what
+Keeps, for every kernel named P... (default "void vip::": the library's) whose launches took
+at least U us (default 5), its last N launches (default 300: the timed region and what
 follows it, after bench.py's clock settle) that overlap no other launch. Writes one row per
 launch: kernel (exact template signature, as vip_launched_kernels names it), index (its
 position among that kernel's launches), duration_ns. The trace's argument list is cut off the
@@ -25,6 +25,7 @@ def main():
     args = sys.argv[1:]
     last = int(args[args.index("--last") + 1]) if "--last" in args else 300
     min_us = float(args[args.index("--min-us") + 1]) if "--min-us" in args else 5.0
+    prefix = args[args.index("--prefix") + 1] if "--prefix" in args else "void vip::"
     rows = list(csv.DictReader(open(args[0])))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), strip_args(r["Kernel_Name"])) for r in rows)
     per = {}
@@ -39,7 +40,7 @@ def main():
         w = csv.writer(fh)
         w.writerow(["kernel", "index", "duration_ns"])
         for n, ds in per.items():
-            if statistics.median(d for d, _ in ds) < min_us * 1e3:
+            if not n.startswith(prefix) or statistics.median(d for d, _ in ds) < min_us * 1e3:
                 continue
             keep = [(i, d) for i, (d, ok) in enumerate(ds) if ok][-last:]
             for i, d in keep:

@@ -275,7 +275,18 @@ def test_launched_prefers_the_multi_frame_form():
 
 ISO_KERNELS = {"c2": ["void vip::bilateral_kernel<7, 16, false, true, 32, 8, 768, false, 16, false>"],
                "c3": ["void vip::adaptive_kernel<7, 16, true, 4, 512, true>"],
-               "c4": ["void vip::bilateral_kernel<4, 16, true, true, 32, 8, 32, true, 16, true>"]}
+               "c4": ["void vip::bilateral_kernel<4, 16, true, true, 32, 8, 32, true, 16, true>"],
+               "c5": ["void vip::bilateral_kernel<15, 16, false, true, 32, 8, 768, false, 16, false>"]}
+
+
+def test_c1_shared_launch_sample():
+    """C1's line takes 3 frames per shared launch on 4 streams: its sample is of that
+    multi-frame kernel, profiled on one stream with the tiling planned for 4 frames in flight
+    (bench.py --batch 3 --frames-in-flight 4), and its PMC summary holds the same kernel."""
+    kern = "void vip::bilateral_frames_kernel<5, 16, false, true, 32, 4, 768, false, 64, false>"
+    s = bench.isolated_sample("c1", kern)
+    assert s is not None and s["launches"] >= 200
+    assert bench.valu_issue("c1", kern, s["mean_us"] / 1e3) is not None
 
 
 @pytest.mark.parametrize("cfg", sorted(ISO_KERNELS))
@@ -307,14 +318,15 @@ def test_isolated_sample_script(tmp_path):
     """scripts/isolated_sample.py keeps the last N non-overlapping launches per kernel above
     the duration floor."""
     import subprocess
-    rows = [("k", i * 100, i * 100 + 50) for i in range(10)] + [("j", 2000, 2001), ("k", 2010, 2100), ("k", 2050, 2150)]
+    rows = [("k", i * 100, i * 100 + 50) for i in range(10)] + [("j", 2000, 2001), ("k", 2010, 2100), ("k", 2050, 2150),
+                                                                ("z(int)", 2200, 2900)]
     f = tmp_path / "t.csv"
     f.write_text("Kernel_Name,Start_Timestamp,End_Timestamp\n" + "".join(f"{n},{s},{e}\n" for n, s, e in rows))
     out = tmp_path / "o.csv"
     subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "isolated_sample.py"), str(f), str(out), "--last", "4",
-                    "--min-us", "0.01"], check=True, capture_output=True)
+                    "--min-us", "0.01", "--prefix", "k"], check=True, capture_output=True)
     import csv
     got = list(csv.DictReader(open(out)))
     assert [int(r["index"]) for r in got if r["kernel"] == "k"] == [6, 7, 8, 9]  # overlapping pair dropped
     assert all(int(r["duration_ns"]) == 50 for r in got if r["kernel"] == "k")
-    assert not [r for r in got if r["kernel"] == "j"]  # below the floor
+    assert not [r for r in got if r["kernel"] in ("j", "z")]  # below the floor; another prefix
