@@ -177,3 +177,53 @@ def test_split_bands_tile_the_own_rows():
                     assert covered == list(range(g.own)), (h, n, r, rank, rows)
                     if ni:
                         assert i0 - r >= 0 and i0 + ni + r <= g.own  # the interior's windows stay in own rows
+
+
+class _InfoShard:
+    """A stand-in for NativeShard.comm_info (what RCCL would report), for the gather logic."""
+
+    def __init__(self, count, user_rank, bus):
+        self.i = dict(count=count, user_rank=user_rank, device=0, pci_bus_id=bus)
+
+    def comm_info(self):
+        return dict(self.i)
+
+
+def _rccl_worker(rank, world, port, mode, out_dir):
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import various_image_processings_amd.sharded as sh
+    sh.rccl_version = lambda: 22606  # no RCCL call without a GPU
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    bus = f"0000:{0x10 + rank:02x}:00.0" if mode != "same_device" else "0000:10:00.0"
+    count = world if mode != "small_comm" else 1
+    user = rank if mode != "small_comm" else 0
+    ev = bench.rccl_evidence([_InfoShard(count, user, bus)] * 2, rank, world, world)
+    with open(os.path.join(out_dir, f"rccl{rank}.json"), "w") as fh:
+        json.dump(ev, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["ok", "same_device", "small_comm"])
+def test_rccl_evidence_gathered_over_gloo(tmp_path, mode):
+    """bench.rccl_evidence at world size 2: every rank sees every rank's RCCL count, user rank
+    and PCI bus id, and flags two ranks on one device or communicators of one rank each (what a
+    line of an 8-GPU run that fell back or doubled up on a device would show)."""
+    import json
+    world = 2
+    mp.spawn(_rccl_worker, args=(world, _free_port(), mode, str(tmp_path)), nprocs=world, join=True)
+    evs = [json.load(open(tmp_path / f"rccl{r}.json")) for r in range(world)]
+    assert evs[0] == evs[1]
+    ev = evs[0]
+    assert [r["rank"] for r in ev["ranks"]] == [0, 1]
+    if mode == "ok":
+        assert ev["problems"] == [] and ev["count"] == 2 and ev["distinct_devices"] == 2
+    elif mode == "same_device":
+        assert ev["distinct_devices"] == 1 and any("distinct devices" in p for p in ev["problems"])
+    else:
+        assert any("expected 2" in p for p in ev["problems"])
