@@ -1326,6 +1326,8 @@ def main():
         out["valid"] = not problems
         if problems:
             out["invalid_reason"] = "; ".join(problems)
+    from various_image_processings_amd import build_info
+    out["build"] = build_info.check()  # the loaded libraries against the sources beside them
     if args.loopback > 1:
         out["rehearsal"] = (f"one GPU: the middle rank's slab of a {args.loopback}-way row split, its two neighbours "
                             f"the rank itself over a one-rank RCCL communicator (vip_shard_create_loopback); value "

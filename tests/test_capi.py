@@ -215,3 +215,17 @@ def test_launch_log_names_kernels_like_the_profiler():
     assert lib.vip_launched_kernels(None, 0) > 0
     assert launched_kernels() == ["void vip::bilateral_kernel<7, 16, false, true, 32, 8, 768, false, 16, false>"]
     assert launched_kernels() == []
+
+
+def test_build_stamp_matches_the_tree():
+    """__graft_entry__.build() stamps the libraries with the sources they were built from
+    (various_image_processings_amd/build_info.json); bench.py reports the check as `build`.
+    In a built tree whose sources are unchanged, the libraries on disk are the stamped ones."""
+    from various_image_processings_amd import build_info
+    c = build_info.check()
+    if c.get("stamp", 1) is None:
+        pytest.skip("not built by __graft_entry__.build() in this tree")
+    assert set(c) >= {"sources_match", "libs_match", "built_utc"}
+    if c["sources_match"]:
+        assert c["libs_match"], c
+    assert len(build_info.source_files()) > 15
