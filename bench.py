@@ -924,16 +924,18 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
                                                round(v, 4)
                                                for (s_, sp_, b_, sh_), v in trial.items()})
         res["halo_batch"] = best_b
-    elif single_batch:
+    elif single_batch or (not multi and len(s_forms) > 1):
         # N = 1, the same (S, B) grid as the N > 1 trial: S frames in flight, B frames per
-        # shared launch. Each form runs as many steps as fill about a quarter of the timed
-        # region (a multiple of every B) after one untimed pass over the buffers; keep the
-        # fastest.
+        # shared launch (the texture filter: S only, one handle per stream). Each form runs
+        # as many steps as fill about a quarter of the timed region (a multiple of every B)
+        # after one untimed pass over the buffers; keep the fastest.
         trial = {}
         n_trial = 6 * max(8, args.steps // 24)
         s_first = sorted(s_forms, key=lambda n: n != args.streams)  # the config's stream count first
         forms = [f for f in cfg.get("single_gpu_forms", single_gpu_forms(s_first, batches))
                  if f[0] <= len(streams) and (batches is None or f[1] in batches)] or single_gpu_forms(s_first, batches)
+        if not single_batch:  # no shared launches: one frame per launch on each stream count
+            forms = [(n, 1) for n in s_first]
         if not forms:
             raise SystemExit(f"bench.py: --batch {args.batch} fits none of the stream counts {s_forms}")
         for n_s, b in forms:
@@ -1196,7 +1198,8 @@ def main():
     frame_h = cfg.get("frame_height") or (per_rank * gw if args.scaling == "weak" else per_rank)
     s_forms = None
     if not fixed_streams and ((sharded and args.exchange == "native") or
-                              (not state["multi"] and cfg["kind"] in FLOP_PER_TAP)):
+                              (not state["multi"] and (cfg["kind"] in FLOP_PER_TAP or
+                                                       (cfg["kind"] == "texture" and args.texture_mode != "fused")))):
         # the trial also picks the frames in flight (TRIAL_STREAMS): at N > 1 native one
         # shard per stream; at N = 1 (plain and adaptive filters) the same S x B grid, so
         # the N = 1 and N > 1 lines are timed in the same forms
