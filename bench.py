@@ -190,12 +190,13 @@ def circle_taps(r: int) -> int:
 CONFIGS = {
     # C1 is the include/cpp (CPU) plumbing case: cpu_baseline times it; the GPU line is
     # the same filter on the same image through the HIP path
-    # c1: 4 frames in flight on 4 streams. The library counts the frames in flight (distinct
+    # c1: 4 frames in flight on 4 streams by default (the trial also tries 2 and 3, with B
+    # frames per shared launch). The library counts the frames in flight (distinct
     # streams among its recent launches) and picks the throughput tiling by itself: 16-wave
     # 256-pixel tiles, 64 workgroups per 512x512 frame, so four frames run side by side (one
     # frame alone takes 256 4-wave tiles, 10.7 against 14.5 us per launch)
     "c1": dict(kind="bilateral", width=512, frame_height=512, ksize=11, data="lenna", cpu_input="lenna",
-               streams=4, kernel="void vip::bilateral_kernel<5, 16,",
+               default_streams=4, kernel="void vip::bilateral_kernel<5, 16,",
                kernel_label="bilateral_kernel<R=5> (16 waves x 256-px tiles, 64 per frame, chosen for 4 frames in flight)",
                workload="bilateral r=5 sigma_s=10 sigma_r=30 lenna 512x512"),
     "c2": dict(kind="bilateral", width=3840, rows_per_rank=2160, ksize=15, workload="bilateral r=7 3840x2160 RGB8"),
@@ -256,7 +257,7 @@ def parse():
     # 0.178 -> 0.173 ms, C3 0.327 -> 0.323, C4 0.717 -> 0.641 ms per frame with 2; 3 no
     # better. S must divide the 12 rotating buffers (a buffer always meets the same stream)
     p.add_argument("--streams", type=int, default=None, choices=[1, 2, 3, 4, 6],
-                   help="default: the config's own (c1 4), else 2; N > 1 native: the trial picks 2, 3 or 4")
+                   help="fixes S; default: the trial picks 2, 3 or 4 (the config's own first: c1 4, else 2)")
     # N>1: "strong" splits the metric's frame (C2/C3: 3840x2160) over the ranks (default
     # for c2, c3, c5), "weak" gives every rank a 2160-row slab of an (N*2160)-row frame
     # (default for c4). A strong c2/c3 line also carries the weak figure ("weak" key)
@@ -1174,8 +1175,8 @@ def main():
 
     if args.frames_in_flight:
         vip.set_bilateral_frames_in_flight(args.frames_in_flight)
-    fixed_streams = args.streams or cfg.get("streams")
-    S = args.streams = fixed_streams or 2
+    fixed_streams = args.streams
+    S = args.streams = fixed_streams or cfg.get("default_streams", 2)
     if "tiling" in cfg and world == 1:  # the config's tile shape (include/vip.h tuning knobs)
         vip.set_bilateral_waves(cfg["tiling"][0])
         vip.set_bilateral_wide(cfg["tiling"][1])
