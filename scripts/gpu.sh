@@ -84,7 +84,8 @@ for step in "$@"; do
           "${A[@]:1}" > $d/p$i.log 2>&1
         rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || fail "$step pass $i" $rc $d/p$i.log
       done
-      python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json | cut -c1-400 || fail "$step" $? ;;
+      fpl=1; for ((j = 1; j < ${#A[@]}; ++j)); do [ "${A[$j]}" = --batch ] && fpl=${A[$((j + 1))]}; done
+      python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json --frames-per-launch $fpl | cut -c1-400 || fail "$step" $? ;;
     rehearse)
       cfg=${A[0]}; n=${A[1]}; sfx=$(printf '%s' "${A[*]:2}" | tr -c 'a-zA-Z0-9' '_'); out=$O/${TAG}_${cfg}_loopback$n$sfx.json
       timeout -k 10 400 python bench.py --config $cfg --rehearse-native --loopback $n --steps 400 "${A[@]:2}" \

@@ -1,7 +1,9 @@
 """Summarise rocprofv3 --pmc passes (scripts/gpu_pmc.sh) into profiles/<tag>_pmc.json.
 
-usage: python scripts/pmc_summary.py gpurun_out/pmc_c2 profiles/r01_c2_pmc.json
-Per kernel: mean of every counter over its dispatches. HBM traffic per launch
+usage: python scripts/pmc_summary.py gpurun_out/pmc_c2 profiles/r01_c2_pmc.json [--frames-per-launch B]
+Per kernel: mean of every counter over its dispatches. A multi-frame kernel
+(`..._frames_kernel<`, bench.py --batch B) carries B frames per dispatch: its entry records
+`frames_per_launch` so that bench.py divides its counts per frame. HBM traffic per launch
 follows MI355X_MICROARCH.md's rocprofv3 section: FETCH_SIZE (KiB) counts 128-B
 memory-side read requests at 64 B on gfx950, so it is doubled; WRITE_SIZE (KiB)
 is taken as is. Both include Infinity-Cache hits (bench.py rotates 12 slabs,
@@ -15,7 +17,7 @@ import os
 import sys
 
 
-def main(src, dst):
+def main(src, dst, fpl=1):
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
         for r in csv.DictReader(open(f)):
@@ -32,6 +34,8 @@ def main(src, dst):
             k["fetch_bytes"] = 2 * means["FETCH_SIZE"] * 1024
             k["write_bytes"] = means["WRITE_SIZE"] * 1024
             k["traffic_bytes"] = k["fetch_bytes"] + k["write_bytes"]
+        if "_frames_kernel<" in name and fpl > 1:
+            k["frames_per_launch"] = fpl
         out["kernels"][name.split("(")[0]] = k
     with open(dst, "w") as fh:
         json.dump(out, fh, indent=1, sort_keys=True)
@@ -41,4 +45,5 @@ def main(src, dst):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:3])
+    a = sys.argv[1:]
+    main(a[0], a[1], int(a[a.index("--frames-per-launch") + 1]) if "--frames-per-launch" in a else 1)
