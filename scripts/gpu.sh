@@ -68,9 +68,12 @@ for step in "$@"; do
       python scripts/kernel_busy.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_busy.json > /dev/null || fail "$step" $?
       head -4 $O/${TAG}_${cfg}_kernel_stats.csv | cut -c1-200 ;;
     iso)
-      cfg=${A[0]}; steps=400; [ $cfg = c5 ] && steps=240; [ $cfg = c4 ] && steps=300; d=$O/iso_${TAG}_$cfg
+      # step counts are multiples of 12, so a --batch B run (B | 12) has no partial batch whose
+      # multi-frame launch would carry fewer frames
+      cfg=${A[0]}; steps=1200; [ $cfg = c5 ] && steps=240; [ $cfg = c4 ] && steps=300; [ $cfg = c2 ] && steps=408
+      [ $cfg = c3 ] && steps=408; d=$O/iso_${TAG}_$cfg
       timeout -k 10 500 rocprofv3 --kernel-trace -d $d -o run --output-format csv -- \
-        python bench.py --config $cfg --streams 1 --batch 1 --steps $steps --warmup 3 --no-cpu-baseline \
+        python bench.py --config $cfg --streams 1 --batch 1 --steps $steps --warmup 12 --no-cpu-baseline \
         "${A[@]:1}" > $d.log 2>&1
       rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
       python scripts/isolated_sample.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_isolated.csv --last 300 \
@@ -80,7 +83,7 @@ for step in "$@"; do
       for set in "${PMC_SETS[@]}"; do
         i=$((i+1))
         timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $set -d $d/p$i -o run --output-format csv -- \
-          python bench.py --config $cfg --streams 1 --batch 1 --steps 5 --warmup 1 --settle-s 0.3 --no-cpu-baseline \
+          python bench.py --config $cfg --streams 1 --batch 1 --steps 12 --warmup 12 --settle-s 0.3 --no-cpu-baseline \
           "${A[@]:1}" > $d/p$i.log 2>&1
         rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || fail "$step pass $i" $rc $d/p$i.log
       done
