@@ -407,11 +407,16 @@ def isolated_sample(config: str, kernel) -> dict | None:
         return None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_isolated.csv")), reverse=True):
         with open(f) as fh:
-            ns = [int(r["duration_ns"]) for r in csv.DictReader(fh) if r["kernel"] == kernel]
-        if ns:
-            return dict(source=os.path.relpath(f, ROOT), launches=len(ns), mean_us=round(sum(ns) / len(ns) / 1e3, 2),
-                        median_us=round(statistics.median(ns) / 1e3, 2), min_us=round(min(ns) / 1e3, 2),
-                        max_us=round(max(ns) / 1e3, 2))
+            rows = [r for r in csv.DictReader(fh) if r["kernel"] == kernel]
+        if rows:
+            ns = [int(r["duration_ns"]) for r in rows]
+            fpl = int(rows[0].get("frames_per_launch") or 1)
+            out = dict(source=os.path.relpath(f, ROOT), launches=len(ns), mean_us=round(sum(ns) / len(ns) / 1e3, 2),
+                       median_us=round(statistics.median(ns) / 1e3, 2), min_us=round(min(ns) / 1e3, 2),
+                       max_us=round(max(ns) / 1e3, 2))
+            if fpl > 1:  # a multi-frame kernel profiled with fpl frames per launch
+                out.update(frames_per_launch=fpl, mean_us_per_frame=round(sum(ns) / len(ns) / 1e3 / fpl, 3))
+            return out
     return None
 
 
@@ -1075,8 +1080,8 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
                 vip_.set_bilateral_frames_in_flight(min(S_run, 4))
                 try:
                     single_ms = one_stream(after + n1 + (-(after + n1)) % B)
-                finally:
-                    vip_.set_bilateral_frames_in_flight(0)
+                finally:  # back to the run's own setting (--frames-in-flight, else counted)
+                    vip_.set_bilateral_frames_in_flight(args.frames_in_flight)
                 res["launch_timing"] = (f"one stream, the tiling planned for the timed region's {S_run} frames in "
                                         f"flight (vip_bilateral_set_frames_in_flight)")
                 if not set(launched_kernels()) <= timed_kernels:
@@ -1263,8 +1268,6 @@ def main():
             if fpl > 1:
                 roof["frames_per_launch"] = fpl
             roof["isolated_sample"] = isolated_sample(args.config, kname)
-            if roof["isolated_sample"] and fpl > 1:  # the sample's launches carry fpl frames each
-                roof["isolated_sample"]["mean_us_per_frame"] = round(roof["isolated_sample"]["mean_us"] / fpl, 2)
             if m["frames_in_flight"] > 1:  # the chip's rate with frames in flight (launches overlap)
                 fl = flops / (ms_per_step * 1e-3) / 1e12
                 roof["in_flight"] = dict(achieved=round(fl, 3), frac=round(fl / PEAK_FP32_TFLOPS, 4), unit="TFLOP/s",

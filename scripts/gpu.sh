@@ -76,8 +76,10 @@ for step in "$@"; do
         python bench.py --config $cfg --streams 1 --batch 1 --steps $steps --warmup 12 --no-cpu-baseline \
         "${A[@]:1}" > $d.log 2>&1
       rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
+      fpl=1; for ((j = 1; j < ${#A[@]}; ++j)); do [ "${A[$j]}" = --batch ] && fpl=${A[$((j + 1))]}; done
       python scripts/isolated_sample.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_isolated.csv --last 300 \
-        || fail "$step" $? ;;
+        --frames-per-launch $fpl || fail "$step" $?
+      rm -rf $d ;;  # the raw trace (tens of MB for a small frame) stays on the box
     pmc)
       cfg=${A[0]}; d=$O/pmc_${TAG}_$cfg; mkdir -p $d; i=0
       for set in "${PMC_SETS[@]}"; do
@@ -88,7 +90,8 @@ for step in "$@"; do
         rc=$?; echo "pmc pass $i rc=$rc"; [ $rc -eq 0 ] || fail "$step pass $i" $rc $d/p$i.log
       done
       fpl=1; for ((j = 1; j < ${#A[@]}; ++j)); do [ "${A[$j]}" = --batch ] && fpl=${A[$((j + 1))]}; done
-      python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json --frames-per-launch $fpl | cut -c1-400 || fail "$step" $? ;;
+      python scripts/pmc_summary.py $d $O/${TAG}_${cfg}_pmc.json --frames-per-launch $fpl | cut -c1-400 || fail "$step" $?
+      rm -rf $d/p*/ ;;  # the per-dispatch counter tables stay on the box
     rehearse)
       cfg=${A[0]}; n=${A[1]}; sfx=$(printf '%s' "${A[*]:2}" | tr -c 'a-zA-Z0-9' '_'); out=$O/${TAG}_${cfg}_loopback$n$sfx.json
       timeout -k 10 400 python bench.py --config $cfg --rehearse-native --loopback $n --steps 400 "${A[@]:2}" \
