@@ -66,6 +66,7 @@ for step in "$@"; do
       rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
       cp $d/run_kernel_stats.csv $O/${TAG}_${cfg}_kernel_stats.csv
       python scripts/kernel_busy.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_busy.json > /dev/null || fail "$step" $?
+      rm -rf $d
       head -4 $O/${TAG}_${cfg}_kernel_stats.csv | cut -c1-200 ;;
     iso)
       # step counts are multiples of 12, so a --batch B run (B | 12) has no partial batch whose
