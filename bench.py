@@ -132,6 +132,11 @@ def _run_ranks(n, argv, timeout_s, script, capture):
     return rc, lines
 
 
+def align(i: int) -> int:
+    """The next step index that starts a whole batch for every B (a multiple of NBUF)."""
+    return i + (-i) % NBUF
+
+
 def halo_batches(streams: int) -> list:
     """Frames per RCCL group the N > 1 native path may use with this many streams: frame i
     runs in batch i // B on stream (i // B) % S, so B * S must divide NBUF for buffer
@@ -872,6 +877,10 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             step(i_settle)
             i_settle += 1
         torch.cuda.synchronize(dev)
+    # every phase below starts on a multiple of NBUF (= 12, a multiple of every B), so its
+    # batches are whole: frames per RCCL group / per shared launch are always B (skipped
+    # indices run nothing; buffer i % NBUF keeps its stream)
+    i_settle = align(i_settle)
     batches = None if args.batch is None else [args.batch]
     if native and not has_peers:
         # one rank (--rehearse-native): no halo moves, so split / batch forms would only
@@ -941,7 +950,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # as many steps as fill about a quarter of the timed region (a multiple of every B)
         # after one untimed pass over the buffers; keep the fastest.
         trial = {}
-        n_trial = 6 * max(8, args.steps // 24)
+        n_trial = NBUF * max(4, args.steps // 48)
         s_first = sorted(s_forms, key=lambda n: n != args.streams)  # the config's stream count first
         forms = [f for f in cfg.get("single_gpu_forms", single_gpu_forms(s_first, batches))
                  if f[0] <= len(streams) and (batches is None or f[1] in batches)] or single_gpu_forms(s_first, batches)
@@ -982,6 +991,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     base = i_settle
     for i in range(args.warmup):
         step(base + i)
+    t_first = align(base + args.warmup)  # the first timed step
     if batching:
         flush()
     torch.cuda.synchronize(dev)
@@ -995,7 +1005,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     for s in streams[1:S_run]:
         s.wait_event(ev0)
     for i in range(args.steps):
-        step(base + args.warmup + i)
+        step(t_first + i)
     if batching:
         flush()  # a partial last batch is part of the timed frames
     host_s = time.perf_counter() - t0  # every step enqueued
@@ -1008,7 +1018,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    after = base + args.warmup + args.steps
+    after = align(t_first + args.steps)
     single_ms = None
     parts = None
     B = hb["B"]
