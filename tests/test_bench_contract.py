@@ -330,3 +330,22 @@ def test_isolated_sample_script(tmp_path):
     assert [int(r["index"]) for r in got if r["kernel"] == "k"] == [6, 7, 8, 9]  # overlapping pair dropped
     assert all(int(r["duration_ns"]) == 50 for r in got if r["kernel"] == "k")
     assert not [r for r in got if r["kernel"] in ("j", "z")]  # below the floor; another prefix
+
+
+def test_aligned_phases_make_whole_batches():
+    """bench.py flushes a batch when (i + 1) % B == 0; every phase (trial form, warm-up,
+    timed steps) starts at align(i), a multiple of NBUF, so with a phase length that B
+    divides every batch has exactly B frames -- the PMC and launch samples of a shared
+    launch then always carry B frames."""
+    for S in (1, 2, 3, 4):
+        for B in bench.halo_batches(S):
+            for start in (0, 5, 13, 1001):
+                i0 = bench.align(start)
+                assert i0 % bench.NBUF == 0 and 0 <= i0 - start < bench.NBUF
+                sizes, pending = [], []
+                for i in range(i0, i0 + 12 * B):
+                    pending.append(i)
+                    if (i + 1) % B == 0:
+                        sizes.append(len(pending))
+                        pending = []
+                assert not pending and set(sizes) == {B}
