@@ -656,6 +656,15 @@ def native_shards(args, cfg, frame_h, rank, world, n):
     return shards, None
 
 
+def device_identity(torch, dev) -> str:
+    """This rank's device as the PCI location torch reports (domain:bus:device), else its
+    uuid, else its index: what tells two ranks' devices apart without an RCCL readback."""
+    p = torch.cuda.get_device_properties(dev)
+    if all(hasattr(p, a) for a in ("pci_domain_id", "pci_bus_id", "pci_device_id")):
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return str(getattr(p, "uuid", None) or f"index {torch.cuda.current_device()}")
+
+
 def rccl_evidence(shards, rank, world, expected_count) -> dict:
     """What RCCL itself reports about the communicators this run exchanged over: every
     rank's ncclCommCount / ncclCommUserRank / ncclCommCuDevice (vip_shard_comm_info, for each
@@ -1343,6 +1352,14 @@ def main():
             problems.append("no RCCL communicator to report (no native shard)")
         if m.get("exchange_fallback"):
             problems.append(f"exchange fell back to torch.distributed P2P: {m['exchange_fallback']}")
+        if not m.get("rccl") and world > 1:
+            # torch P2P exchange (or a fallback): no RCCL readback, but the ranks' devices
+            # must still be distinct (the --same-device gloo rehearsal is not an N-GPU run)
+            ids = [None] * world
+            dist.all_gather_object(ids, device_identity(torch, dev))
+            out["devices"] = ids
+            if len(set(ids)) != world:
+                problems.append(f"{world} ranks on {len(set(ids))} distinct devices")
         if world != args.gpus:
             problems.append(f"--gpus {args.gpus} but {world} rank(s) ran")
         out["valid"] = not problems
