@@ -28,8 +28,15 @@ communicators, one per stream), then filter their own rows.
 Inputs are synthetic (test/random_array-style uniform u8), resident in HBM before
 timing; 12 distinct input/output slabs rotate so the working set exceeds the
 256 MB Infinity Cache. Rank 0 prints ONE JSON line. The roofline object is for
-the dominant kernel, timed with HIP events on the stream it runs on; the CPU
+the dominant kernel, timed with HIP events on the stream it runs on, beside the
+committed single-stream rocprofv3 launch sample of the same instantiation; the CPU
 baseline (rank 0, N=1) is the oracle's include/cpp restatement on the host cores.
+
+Before the timed steps a trial picks how frames overlap, with the same grid at every N:
+S streams x B frames per shared launch (N = 1) or per RCCL group (N > 1, where the trial
+also crosses the interior/edge split and the CUs a shared launch leaves free); the line
+reports `frames_in_flight` (S x B) and `frame_latency_ms`. An N > 1 line carries `rccl`
+(what RCCL reports about every rank's communicators and devices) and `valid`.
 """
 from __future__ import annotations
 
