@@ -164,7 +164,8 @@ int vip_shard_rccl_version(int* version);
 
 /* What the shard's RCCL communicator reports about itself (ncclCommCount,
  * ncclCommUserRank, ncclCommCuDevice): ranks in the communicator, this shard's rank in it,
- * its HIP device. A loopback shard reports 1 / 0 / the current device. */
+ * its HIP device. A loopback shard reports 1 / 0 / the current device; a LOCAL shard has no
+ * communicator (VIP_ERR_INVALID_ARGUMENT). */
 int vip_shard_comm_info(vip_shard_t h, int* count, int* user_rank, int* device);
 
 /* PCI bus id ("dddd:bb:dd.f") of the shard's device (hipDeviceGetPCIBusId); len >= 13. */
