@@ -141,25 +141,10 @@ inline int device_cus() {
 }
 
 // free_cus: CUs the launch leaves to concurrent work (StencilArgs::free_cus)
-// Workgroups of a persistent launch (one per CU, less free_cus). With R = ceil(tiles / cus)
-// rounds the launch lasts R tile-times however many workgroups share the tiles, so it takes
-// only ceil(tiles / R) of them (rounded up to a multiple of 8: every XCD gets as many and
-// the XCD tile map stays on) and leaves the other CUs to concurrent launches -- another
-// stream's frames, the RCCL exchange kernels. E.g. six 270-row slabs of the 4K frame on
-// wide tiles, 1,530 tiles with 8 CUs free: 7 rounds either way, 224 workgroups instead of
-// 248. VIP_PERSISTENT_BALANCE=0 restores one workgroup on every available CU (measurement).
 inline int persistent_blocks(int tiles, int free_cus = 0) {
     int cus = device_cus() - (free_cus > 0 ? free_cus : 0);
     cus = cus > 0 ? cus : 1;
-    if (tiles <= cus) return tiles;
-    static const bool balance = [] {
-        const char* v = std::getenv("VIP_PERSISTENT_BALANCE");
-        return !(v && v[0] == '0');
-    }();
-    if (!balance) return cus;
-    const int rounds = (tiles + cus - 1) / cus;
-    const int b = ((tiles + rounds - 1) / rounds + 7) & ~7;
-    return b < cus ? b : cus;
+    return tiles < cus ? tiles : cus;
 }
 
 constexpr int lut_words(bool adaptive) { return adaptive ? 1536 * 16 : 768 * 32; }
