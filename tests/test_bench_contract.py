@@ -349,3 +349,25 @@ def test_aligned_phases_make_whole_batches():
                         sizes.append(len(pending))
                         pending = []
                 assert not pending and set(sizes) == {B}
+
+
+def test_pmc_summary_records_frames_per_launch(tmp_path):
+    """scripts/pmc_summary.py --frames-per-launch B marks the multi-frame kernels of a
+    `bench.py --batch B` pass, and bench.py divides their counts and bytes per frame."""
+    import subprocess
+    d = tmp_path / "pmc"
+    (d / "p1").mkdir(parents=True)
+    rows = [("void vip::bilateral_frames_kernel<5, 16>(vip::StencilArgs)", "SQ_INSTS_VALU", 3000.0),
+            ("void vip::bilateral_kernel<5, 16>(vip::StencilArgs)", "SQ_INSTS_VALU", 1000.0),
+            ("void vip::bilateral_frames_kernel<5, 16>(vip::StencilArgs)", "FETCH_SIZE", 30.0),
+            ("void vip::bilateral_frames_kernel<5, 16>(vip::StencilArgs)", "WRITE_SIZE", 60.0)]
+    (d / "p1" / "run_counter_collection.csv").write_text(
+        "Kernel_Name,Counter_Name,Counter_Value\n" + "".join(f'"{k}",{c},{v}\n' for k, c, v in rows))
+    out = tmp_path / "r99_cx_pmc.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_summary.py"), str(d), str(out),
+                    "--frames-per-launch", "3"], check=True, capture_output=True)
+    k = json.loads(out.read_text())["kernels"]
+    assert k["void vip::bilateral_frames_kernel<5, 16>"]["frames_per_launch"] == 3
+    assert "frames_per_launch" not in k["void vip::bilateral_kernel<5, 16>"]
+    e = k["void vip::bilateral_frames_kernel<5, 16>"]
+    assert e["traffic_bytes"] == (2 * 30 + 60) * 1024
