@@ -9,6 +9,16 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
+
+#define HC(x)                                                               \
+    do {                                                                    \
+        const hipError_t e_ = (x);                                          \
+        if (e_ != hipSuccess) {                                             \
+            std::printf("%s -> %s\n", #x, hipGetErrorString(e_));          \
+            std::exit(1);                                                   \
+        }                                                                   \
+    } while (0)
 
 #include "vip_stencil.hpp"
 
@@ -74,22 +84,22 @@ __global__ __launch_bounds__(1024) void rate(float* out, float seed) {
 template <int KIND>
 void run(const char* name, float* d) {
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    HC(hipEventCreate(&e0));
+    HC(hipEventCreate(&e1));
     for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(rate<KIND>, dim3(256), dim3(1024), 0, 0, d, 3.f);
-    hipEventRecord(e0);
+    HC(hipEventRecord(e0));
     for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(rate<KIND>, dim3(256), dim3(1024), 0, 0, d, 3.f);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
+    HC(hipEventRecord(e1));
+    HC(hipEventSynchronize(e1));
     float ms;
-    hipEventElapsedTime(&ms, e0, e1);
+    HC(hipEventElapsedTime(&ms, e0, e1));
     const double evals = 5.0 * 256 * 16 * ITERS * 8 / 1024.0;  // wave-evaluations per SIMD
     printf("%-58s %8.3f ms  %.3f ns per wave-evaluation per SIMD\n", name, ms / 5, ms * 1e6 / evals);
 }
 
 int main() {
     float* d;
-    hipMalloc(&d, 256 * 1024 * sizeof(float));
+    HC(hipMalloc(&d, 256 * 1024 * sizeof(float)));
     run<0>("exp_tab_f32 (shipped: f64, 64-entry double table)", d);
     run<1>("float-float candidate (f32 ops, Ziv test, no fallback)", d);
     run<2>("v_exp_f32 (hardware, inexact: lower bound)", d);

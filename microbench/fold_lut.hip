@@ -21,6 +21,16 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+
+#define HC(x)                                                               \
+    do {                                                                    \
+        const hipError_t e_ = (x);                                          \
+        if (e_ != hipSuccess) {                                             \
+            std::printf("%s -> %s\n", #x, hipGetErrorString(e_));          \
+            std::exit(1);                                                   \
+        }                                                                   \
+    } while (0)
 #include <vector>
 
 #define ITERS 384
@@ -109,20 +119,20 @@ __global__ __launch_bounds__(1024) void taps(float* out, const float* __restrict
 template <int KIND>
 double run(const char* name, float* d_out, const float* d_lut, const float* d_ws) {
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    HC(hipEventCreate(&e0));
+    HC(hipEventCreate(&e1));
     const int blocks = 256;
-    hipFuncSetAttribute(reinterpret_cast<const void*>(taps<KIND>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        kLdsBytes);
+    HC(hipFuncSetAttribute(reinterpret_cast<const void*>(taps<KIND>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           kLdsBytes));
     for (int w = 0; w < 2; ++w) hipLaunchKernelGGL(taps<KIND>, dim3(blocks), dim3(1024), kLdsBytes, 0, d_out, d_lut, d_ws);
-    hipEventRecord(e0);
+    HC(hipEventRecord(e0));
     const int reps = 5;
     for (int r = 0; r < reps; ++r)
         hipLaunchKernelGGL(taps<KIND>, dim3(blocks), dim3(1024), kLdsBytes, 0, d_out, d_lut, d_ws);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
+    HC(hipEventRecord(e1));
+    HC(hipEventSynchronize(e1));
     float ms;
-    hipEventElapsedTime(&ms, e0, e1);
+    HC(hipEventElapsedTime(&ms, e0, e1));
     // wave-taps per SIMD: blocks * 16 waves * ITERS * kTaps * 8 outputs / 1024 SIMDs
     const double wave_taps = (double)blocks * 16 * ITERS * kTaps * 8 / 1024.0;
     const double ns = ms / reps * 1e6 / wave_taps;
@@ -137,11 +147,11 @@ int main() {
     for (int i = 0; i < kLutWords; ++i) lut[i] = std::exp(-(float)((i / 32) % 768) * ((i / 32) % 768) / 1800.f);
     for (int k = 0; k < kClasses; ++k) ws[k] = std::exp(-(float)k / 200.f);
     float *d_out, *d_lut, *d_ws;
-    hipMalloc(&d_out, 256 * 1024 * sizeof(float));
-    hipMalloc(&d_lut, lut.size() * sizeof(float));
-    hipMalloc(&d_ws, ws.size() * sizeof(float));
-    hipMemcpy(d_lut, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice);
-    hipMemcpy(d_ws, ws.data(), ws.size() * sizeof(float), hipMemcpyHostToDevice);
+    HC(hipMalloc(&d_out, 256 * 1024 * sizeof(float)));
+    HC(hipMalloc(&d_lut, lut.size() * sizeof(float)));
+    HC(hipMalloc(&d_ws, ws.size() * sizeof(float)));
+    HC(hipMemcpy(d_lut, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice));
+    HC(hipMemcpy(d_ws, ws.data(), ws.size() * sizeof(float), hipMemcpyHostToDevice));
     const double a = run<0>("today: 32-copy LUT, sad lshl_or ds_read mul 3fma add", d_out, d_lut, d_ws);
     const double b = run<1>("folded: 1-copy class tables, sad mad_u16 ds_read 3fma add", d_out, d_lut, d_ws);
     const double a2 = run<0>("today again", d_out, d_lut, d_ws);
