@@ -259,18 +259,22 @@ namespace vip {
 // Guide tile (TW x TH outputs) and workgroup size, per radius. The phases run one
 // work item per thread where the counts allow it: 4 vertically adjacent blur
 // positions per pass-2 run, 4 vertically adjacent guide outputs per guide run, so a
-// (TW + 2R) x (TH + 2R) blur region of 1024 pass-2 runs fills 1024 threads once.
-// 124 x 28 at R = 2 (k = 5, C4): 128 x 32 blur positions = 1024 pass-2 runs, 868
-// guide runs, 79 KiB of LDS -> two 16-wave workgroups per CU, 60 VGPRs. Measured per
-// 4K iteration (guide stage + JBF, profiles/r02_variants.txt): 64 x 16 / 256 threads
-// 158.4-159.7 us, 124 x 28 / 1024 150.3-150.7 us (60 x 60: 157.5, 28 x 124: 154.2,
-// 252 x 12: 177.0, 60 x 28 / 512: 165.3). VIP_GF_TW / _TH / _NT override R <= 2.
+// (TW + 2R) x (TH + 2R) blur region of up to 1024 pass-2 runs fills 1024 threads once.
+// 92 x 36 at R = 2 (k = 5, C4): 96 x 40 blur positions = 960 pass-2 runs (1.159 per
+// output), 828 guide runs, 2160 = 60 tile rows exactly, 75 KiB of LDS -> two 16-wave
+// workgroups per CU. Measured per 4K iteration (guide stage + JBF, round 2,
+// profiles/r02_variants.txt): 64 x 16 / 256 threads 158.4-159.7 us, 124 x 28 / 1024
+// 150.3-150.7 us (60 x 60: 157.5, 28 x 124: 154.2, 252 x 12: 177.0, 60 x 28 / 512: 165.3);
+// round 5, per C4 frame on one stream, interleaved on one box
+// (profiles/r05_gf_tiles_{a,b,c}.txt): 92 x 36 656.1-661.0 us against 124 x 28
+// 661.7-667.2 (96 x 36 668-671, 124 x 24 673, 108 x 32 678-680, 80 x 40 697, 80 x 44 692,
+// 60 x 60 693). VIP_GF_TW / _TH / _NT override R <= 2.
 struct GfTile { int tw, th, nt; };
 constexpr GfTile gf_tile(int R) {
 #if defined(VIP_GF_TW) && defined(VIP_GF_TH) && defined(VIP_GF_NT)
     return R <= 2 ? GfTile{VIP_GF_TW, VIP_GF_TH, VIP_GF_NT} : GfTile{64, 16, 256};
 #else
-    return R <= 2 ? GfTile{124, 28, 1024} : GfTile{64, 16, 256};
+    return R <= 2 ? GfTile{92, 36, 1024} : GfTile{64, 16, 256};
 #endif
 }
 constexpr int kGfH1 = 8;   // pass 1: horizontally adjacent window aggregates per thread
