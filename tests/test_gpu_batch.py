@@ -87,3 +87,40 @@ def test_batch_rejects_aliasing_and_handles_empty(dev, oracle):
     impl.run_rows_batch([], [], rows, 0, 0, rows)  # nothing to do
     with pytest.raises(ValueError):
         impl.run_rows_batch([a], [], rows, 0, 0, rows)
+
+
+@pytest.mark.parametrize("kind,k,w,own,inflight", [("bilateral", 15, 3840, 270, 1), ("bilateral", 15, 3840, 270, 2),
+                                                   ("adaptive", 15, 3840, 270, 0), ("bilateral", 5, 1000, 97, 1),
+                                                   ("adaptive", 9, 1000, 97, 0)])
+def test_batch_last_round_pieces(dev, oracle, kind, k, w, own, inflight):
+    """A multi-frame launch cuts its last round's tiles into pieces of a tile's waves, so
+    that more workgroups share that round (plan_tail, vip_stencil.hpp; the plain bilateral
+    only with one frame in flight, forced here both ways). Swept over workgroup counts
+    (free_cus) to get last rounds of many sizes and piece counts: every frame of a 6-frame
+    launch equals its one-frame launch (which never cuts a tile), and frame 0 the oracle."""
+    import various_image_processings_amd as vip
+    if inflight:
+        vip.set_bilateral_frames_in_flight(inflight)
+    try:
+        _last_round_pieces(dev, oracle, kind, k, w, own)
+    finally:
+        vip.set_bilateral_frames_in_flight(0)
+
+
+def _last_round_pieces(dev, oracle, kind, k, w, own):
+    r = k // 2
+    rows = own + 2 * r
+    imgs = _slabs(oracle, 6, w, rows)
+    impl = (_BilateralImpl if kind == "bilateral" else _AdaptiveImpl)(w, rows, k)
+    srcs = [dev.put(x) for x in imgs]
+    want = []
+    for f in range(6):
+        one = dev.empty((own, w, 3))
+        impl.run_rows(srcs[f], one, own, r, 0, rows)
+        want.append(dev.get(one))
+    assert np.array_equal(want[0], (oracle.bilateral if kind == "bilateral" else oracle.adaptive)(imgs[0], k)[r:r + own])
+    for free in (0, 3, 8, 29, 64, 130, 200, 251, 255):
+        dsts = [dev.empty((own, w, 3)) for _ in range(6)]
+        impl.run_rows_batch(srcs, dsts, own, r, 0, rows, free_cus=free)
+        for f in range(6):
+            assert np.array_equal(dev.get(dsts[f]), want[f]), f"free_cus {free} frame {f}"

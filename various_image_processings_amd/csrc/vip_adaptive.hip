@@ -84,12 +84,13 @@ __device__ __forceinline__ void adaptive_body(const StencilArgs& a) {
 #endif
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
-    int tile = blockIdx.x;  // persistent: tiles blockIdx.x + k * gridDim.x
+    int tile = blockIdx.x;  // persistent: items blockIdx.x + k * gridDim.x (item_tile)
+    const int items = launch_items<MULTI>(a);
     TilePrefetch<R, ROWS, NT, P> pf;
     LutStage<NT, NE, COPIES> ls;  // LUT reads go out before the first tile's
     ls.load(a.color);
     {  // multi-frame launches: frame f's tiles follow frame f - 1's
-        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, item_tile<MULTI>(a, tile));
         pf.issue(frame_src<MULTI>(a.src, ft.f), a.src_pitch, a, (ft.t % a.tiles_x) * G::TW, (ft.t / a.tiles_x) * TH);
     }
     ls.store(lut);
@@ -97,11 +98,11 @@ __device__ __forceinline__ void adaptive_body(const StencilArgs& a) {
     __syncthreads();
 
     while (true) {
-        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, item_tile<MULTI>(a, tile));
         const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
-        if (next < a.tiles_total) {
-            const FrameTile fn = frame_tile<MULTI>(a, xcd_tile(next, a.tiles_total));
+        if (next < items) {
+            const FrameTile fn = frame_tile<MULTI>(a, item_tile<MULTI>(a, next));
             pf.issue(frame_src<MULTI>(a.src, fn.f), a.src_pitch, a, (fn.t % a.tiles_x) * G::TW,
                      (fn.t / a.tiles_x) * TH);
         }
@@ -127,7 +128,7 @@ __device__ __forceinline__ void adaptive_body(const StencilArgs& a) {
             }
             __syncthreads();
         }
-        if (ty0 + wave * 4 < a.out_rows) {
+        if (ty0 + wave * 4 < a.out_rows && item_wave<MULTI, WAVES>(a, tile, wave)) {
             uint32_t ctr[P];
             {
                 const uint4* c = reinterpret_cast<const uint4*>(plane + (ty + R) * G::S + tx * P + G::L);
@@ -294,7 +295,7 @@ __device__ __forceinline__ void adaptive_body(const StencilArgs& a) {
             finish_outputs(a01, a2k, o);
             store_px_to(a, frame_dst<MULTI>(a, tile), ty0 + ty, tx0 + tx * P, o);
         }
-        if (next >= a.tiles_total) break;
+        if (next >= items) break;
         __syncthreads();
         pf.commit(plane);
         __syncthreads();
@@ -354,6 +355,10 @@ static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     args.tiles_total = args.tiles_frame * (multi ? a.nframes : 1);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
+    // the last round in pieces (C3 slab at 8 GPUs, 6 frames per launch, 8 CUs free: one
+    // stream 0.0500 -> 0.0477 ms per frame, two streams 0.0429-0.0430 both ways; at 4 GPUs
+    // on two streams 0.0960 -> 0.0939; profiles/r05_slab_batch_ab{,2}.txt)
+    if (multi) plan_tail(args, blocks, WAVES);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }

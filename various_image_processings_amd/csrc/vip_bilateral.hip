@@ -109,8 +109,10 @@ __device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
     const char* const lut_bytes = reinterpret_cast<const char*>(lut);
 
     VIP_RT_STAMP(0);
-    // persistent: workgroup b filters tiles b, b + grid, b + 2 grid, ...
+    // persistent: workgroup b filters items b, b + grid, b + 2 grid, ... (item_tile: the
+    // tiles; in a multi-frame launch the last round's tiles in pieces, plan_tail)
     int tile = blockIdx.x;
+    const int items = launch_items<MULTI>(a);
     TilePrefetch<R, ROWS, NT, P, TPR> pg, ps;
     // once per workgroup; its reads go out first
     std::conditional_t<SAT, SatStage<NT, SL>, LutStage<NT, NTAB * NE, COPIES>> ls;
@@ -118,7 +120,7 @@ __device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
     // multi-frame launches (plain filter only: guide == src): frame f's tiles follow
     // frame f - 1's, so a workgroup's next tile may be the next frame's
     {
-        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, item_tile<MULTI>(a, tile));
         const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         pg.issue(JOINT ? a.guide : frame_src<MULTI>(a.guide, ft.f), a.guide_pitch, a, tx0, ty0);
         if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, tx0, ty0);
@@ -130,16 +132,17 @@ __device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
 
     for ([[maybe_unused]] int it = 0;; ++it) {
         VIP_STAMP(it, 0);
-        const FrameTile ft = frame_tile<MULTI>(a, xcd_tile(tile, a.tiles_total));
+        const FrameTile ft = frame_tile<MULTI>(a, item_tile<MULTI>(a, tile));
         const int tx0 = (ft.t % a.tiles_x) * G::TW, ty0 = (ft.t / a.tiles_x) * TH;
         const int next = tile + (int)gridDim.x;
-        if (next < a.tiles_total) {  // next tile's HBM reads fly under this tile's taps
-            const FrameTile fn = frame_tile<MULTI>(a, xcd_tile(next, a.tiles_total));
+        if (next < items) {  // next tile's HBM reads fly under this tile's taps
+            const FrameTile fn = frame_tile<MULTI>(a, item_tile<MULTI>(a, next));
             const int nx0 = (fn.t % a.tiles_x) * G::TW, ny0 = (fn.t / a.tiles_x) * TH;
             pg.issue(JOINT ? a.guide : frame_src<MULTI>(a.guide, fn.f), a.guide_pitch, a, nx0, ny0);
             if constexpr (JOINT) ps.issue(a.src, a.src_pitch, a, nx0, ny0);
         }
-        if (ty0 + wave * G::RPW < a.out_rows) {  // wave-uniform: skip rows past the frame
+        // wave-uniform: skip rows past the frame, and other pieces' rows of a split tile
+        if (ty0 + wave * G::RPW < a.out_rows && item_wave<MULTI, WAVES>(a, tile, wave)) {
             uint32_t ctr[P];  // centre pixels of the guide (== src for the plain filter)
             {
                 const uint4* c = reinterpret_cast<const uint4*>(gplane + (ty + R) * G::S + tx * P + G::L);
@@ -189,7 +192,7 @@ __device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
             store_px_to(a, JOINT ? a.dst : frame_dst<MULTI>(a, tile), ty0 + ty, tx0 + tx * P, o);
         }
         VIP_STAMP(it, 1);
-        if (next >= a.tiles_total) {
+        if (next >= items) {
             VIP_RT_STAMP(1);
             break;
         }
@@ -404,6 +407,12 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     args.tiles_total = args.tiles_frame * (multi ? a.nframes : 1);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
+    // the last round in pieces for one frame in flight only: with two streams the other
+    // stream's launch already fills the CUs a whole-tile last round leaves idle, and the
+    // pieces' fewer waves per CU cost more CU time (C2 slab at 8 GPUs, 6 frames per launch,
+    // 8 CUs free: one stream 0.0256-0.0258 -> 0.0250 ms per frame, two streams 0.0222-0.0225
+    // -> 0.0231-0.0233; profiles/r05_slab_batch_ab{,2}.txt)
+    if (multi && a.inflight <= 1) plan_tail(args, blocks, WAVES);
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }

@@ -161,6 +161,8 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.nframes = 1;
     a.tiles_frame = 0;
     a.free_cus = 0;
+    a.tail_full = 0;
+    a.tail_shift = 0;
     for (int f = 0; f < kMaxBatchFrames; ++f) {
         a.fsrc[f] = src;
         a.fdst[f] = dst;

@@ -100,6 +100,10 @@ struct StencilArgs {
     int nframes;
     int tiles_frame;       // tiles per frame (set by the launcher)
     int free_cus;          // host only: persistent workgroups leave this many CUs to concurrent work
+    // Last-round split (multi-frame kernels, plan_tail): launch tiles [tail_full, tiles_total)
+    // run in the last round as 2^tail_shift pieces each, a piece being a run of the tile's
+    // waves; tail_full == tiles_total and tail_shift == 0 when the rounds come out even.
+    int tail_full, tail_shift;
     const uint8_t* fsrc[kMaxBatchFrames];
     uint8_t* fdst[kMaxBatchFrames];
     float ws[kWsStride * kWsStride];  // spatial LUT, |ky|-major, in the kernarg segment (scalar loads)
@@ -148,6 +152,28 @@ inline int persistent_blocks(int tiles, int free_cus = 0) {
 }
 
 constexpr int lut_words(bool adaptive) { return adaptive ? 1536 * 16 : 768 * 32; }
+
+#ifndef VIP_TAIL_SPLIT  // build knob: 0 runs the last round's tiles whole
+#define VIP_TAIL_SPLIT 1
+#endif
+// A persistent launch of T tiles on B workgroups runs ceil(T / B) rounds; when the last
+// holds k = T mod B tiles, B - k workgroups idle through it while k run a whole tile each
+// (a C2 slab batch at 8 GPUs: 1,530 tiles on 248 workgroups, 6.17 rounds run as 7). The
+// last round's tiles are cut into m = 2^s pieces of WAVES / m waves each, the largest m
+// with k * m <= B, so that k * m workgroups share them; a piece's workgroup still loads
+// the whole tile plane (the apron rows its waves read) and its other waves skip the taps.
+inline void plan_tail(StencilArgs& a, int blocks, int waves) {
+    a.tail_full = a.tiles_total;
+    a.tail_shift = 0;
+    if (!VIP_TAIL_SPLIT || blocks <= 0) return;
+    const int k = a.tiles_total % blocks;
+    if (k == 0) return;
+    int s = 0;
+    while ((2 << s) <= waves && (static_cast<long long>(k) << (s + 1)) <= blocks) ++s;
+    if (s == 0) return;
+    a.tail_full = a.tiles_total - k;
+    a.tail_shift = s;
+}
 
 // Tile filtered by a persistent workgroup at `slot` (= blockIdx.x + k * gridDim.x, round
 // k). In full rounds each XCD (workgroups are dispatched round-robin over the 8 XCDs,
@@ -718,14 +744,38 @@ __device__ __forceinline__ T kernarg_at(size_t byte_offset) {
     return *(kT*)(base + byte_offset);
 }
 
-// Output base of launch tile `tile`'s frame, derived again at the store: keeping the frame
+// Work items of a persistent launch: the tiles of the full rounds, then the last round's
+// tiles in 2^tail_shift pieces each (plan_tail; one-frame kernels: the tiles).
+template <bool MULTI>
+__device__ __forceinline__ int launch_items(const StencilArgs& a) {
+    if constexpr (!MULTI) return a.tiles_total;
+    return a.tail_full + ((a.tiles_total - a.tail_full) << a.tail_shift);
+}
+// Launch tile of item v (the XCD map in full rounds, the identity in the last)
+template <bool MULTI>
+__device__ __forceinline__ int item_tile(const StencilArgs& a, int v) {
+    if constexpr (!MULTI) return xcd_tile(v, a.tiles_total);
+    return v < a.tail_full ? xcd_tile(v, a.tiles_total) : a.tail_full + ((v - a.tail_full) >> a.tail_shift);
+}
+// Does wave `wave` of a WAVES-wave workgroup filter item v? Every wave of a whole tile; of
+// a last-round piece p, waves [p * WAVES / m, (p + 1) * WAVES / m). Wave-uniform.
+template <bool MULTI, int WAVES>
+__device__ __forceinline__ bool item_wave(const StencilArgs& a, int v, int wave) {
+    if constexpr (!MULTI) return true;
+    if (v < a.tail_full) return true;
+    const int span = WAVES >> a.tail_shift;
+    const int piece = (v - a.tail_full) & ((1 << a.tail_shift) - 1);
+    return static_cast<unsigned>(wave - piece * span) < static_cast<unsigned>(span);
+}
+
+// Output base of item `item`'s frame, derived again at the store: keeping the frame
 // index live across the tap loop costs scalar registers the loop's spatial weights use
 // (measured +1 % on the 4K r=7 launch).
 template <bool MULTI>
-__device__ __forceinline__ uint8_t* frame_dst(const StencilArgs& a, int tile) {
+__device__ __forceinline__ uint8_t* frame_dst(const StencilArgs& a, int item) {
     if constexpr (!MULTI) return a.dst;
-    __asm__ volatile("" : "+s"(tile));  // recompute here, not from the tile's start
-    int mt = xcd_tile(tile, a.tiles_total), f = 0;
+    __asm__ volatile("" : "+s"(item));  // recompute here, not from the tile's start
+    int mt = item_tile<MULTI>(a, item), f = 0;
     while (mt >= a.tiles_frame && a.tiles_frame > 0 && f < kMaxBatchFrames - 1) {
         mt -= a.tiles_frame;
         ++f;
