@@ -162,16 +162,21 @@ constexpr int lut_words(bool adaptive) { return adaptive ? 1536 * 16 : 768 * 32;
 // last round's tiles are cut into m = 2^s pieces of WAVES / m waves each, the largest m
 // with k * m <= B, so that k * m workgroups share them; a piece's workgroup still loads
 // the whole tile plane (the apron rows its waves read) and its other waves skip the taps.
-inline void plan_tail(StencilArgs& a, int blocks, int waves) {
-    a.tail_full = a.tiles_total;
-    a.tail_shift = 0;
-    if (!VIP_TAIL_SPLIT || blocks <= 0) return;
-    const int k = a.tiles_total % blocks;
-    if (k == 0) return;
+// m divides WAVES (a 12-wave tile is cut in 2 or 4, never 8). Returns s (0: no cut).
+constexpr int tail_shift(int tiles, int blocks, int waves) {
+    if (blocks <= 0 || tiles % blocks == 0) return 0;
+    const long long k = tiles % blocks;
     int s = 0;
-    while ((2 << s) <= waves && (static_cast<long long>(k) << (s + 1)) <= blocks) ++s;
-    if (s == 0) return;
-    a.tail_full = a.tiles_total - k;
+    while (waves % (2 << s) == 0 && (k << (s + 1)) <= blocks) ++s;
+    return s;
+}
+static_assert(tail_shift(1530, 248, 16) == 2, "C2 slab batch at 8 GPUs: 42 tiles in 4 pieces");
+static_assert(tail_shift(1530, 255, 16) == 0 && tail_shift(100, 100, 16) == 0, "even rounds: no cut");
+static_assert(tail_shift(7 + 2 * 256, 256, 16) == 4 && tail_shift(7 + 2 * 256, 256, 12) == 2, "pieces divide WAVES");
+static_assert(tail_shift(200 + 256, 256, 16) == 0, "k > blocks / 2: whole tiles");
+inline void plan_tail(StencilArgs& a, int blocks, int waves) {
+    const int s = VIP_TAIL_SPLIT ? tail_shift(a.tiles_total, blocks, waves) : 0;
+    a.tail_full = s ? a.tiles_total - a.tiles_total % blocks : a.tiles_total;
     a.tail_shift = s;
 }
 
