@@ -7,8 +7,12 @@ widths, widths that are not a multiple of any tile), ksize, sigma_space, sigma_c
 drawn over decades), the numerics profile, the input statistics (uniform, narrow
 [100, 120) as sample/benchmark/main.cpp:213 uses, a smooth ramp), and -- through the C
 ABI's pitch argument -- row padding. 48 cases, each small enough for the oracle to finish
-in well under a second.
+in well under a second; a second sweep drives the multi-frame launches (run_rows_batch: row
+bands of 2-6 frames, free CUs, frames in flight, and so the cut last round). VIP_FUZZ_CASES /
+VIP_FUZZ_BATCH_CASES widen the sweeps for a one-off run (profiles/r05_fuzz_wide.log).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -17,7 +21,8 @@ from various_image_processings_amd import _lib
 
 pytestmark = pytest.mark.gpu
 
-N_CASES = 48
+N_CASES = int(os.environ.get("VIP_FUZZ_CASES", 48))
+N_BATCH_CASES = int(os.environ.get("VIP_FUZZ_BATCH_CASES", 24))
 
 
 def _case(i):
@@ -105,3 +110,42 @@ def test_random_case_bit_exact(dev, oracle, i):
     d = np.argwhere(got != want)
     assert not len(d), f"{c}: {len(d)} mismatches, first {d[:3].tolist()}"
     assert (tail == 0x5A).all(), f"{c}: the row padding of the output was written"
+
+
+def _batch_case(i):
+    r = np.random.default_rng(5000 + i)
+    kind = ["bilateral", "adaptive"][i % 2]
+    k = int(r.choice([1, 3, 5, 7, 9, 11, 13, 15, 17]))  # the multi-frame kernels' radii (<= 8)
+    h, w = int(r.integers(1, 200)), int(r.integers(1, 700))
+    row0 = int(r.integers(0, h))
+    out_rows = int(r.integers(1, h - row0 + 1))
+    return dict(kind=kind, k=k, h=h, w=w, row0=row0, out_rows=out_rows, n=int(r.integers(2, 7)),
+                free=int(r.choice([0, 0, 8, 16, 64, int(r.integers(0, 256))])), inflight=int(r.integers(0, 3)),
+                ss=float(10 ** r.uniform(-0.5, 2.5)), sc=float(10 ** r.uniform(-0.3, 2.3)),
+                profile=int(r.integers(0, 2)), seed=5000 + i)
+
+
+@pytest.mark.parametrize("i", range(N_BATCH_CASES))
+def test_random_batch_case_bit_exact(dev, oracle, i):
+    """n frames in one multi-frame launch (include/vip.h vip_*_run_rows_batch), output rows
+    [row0, row0 + out_rows) of each, neighbours clamped to the frame: each equals the
+    oracle's filter of that frame, those rows."""
+    c = _batch_case(i)
+    numerics = vip.VIP_NUMERICS_CPP if c["profile"] else vip.VIP_NUMERICS_CUDA
+    r = np.random.default_rng(c["seed"])
+    imgs = [r.integers(0, 255, (c["h"], c["w"], 3), dtype=np.uint8) for _ in range(c["n"])]
+    cls = vip.filters._BilateralImpl if c["kind"] == "bilateral" else vip.filters._AdaptiveImpl
+    impl = cls(c["w"], c["h"], c["k"], c["ss"], c["sc"], numerics)
+    srcs = [dev.put(x) for x in imgs]
+    dsts = [dev.empty((c["out_rows"], c["w"], 3)) for _ in imgs]
+    vip.set_bilateral_frames_in_flight(c["inflight"])
+    try:
+        impl.run_rows_batch(srcs, dsts, c["out_rows"], c["row0"], 0, c["h"], free_cus=c["free"])
+    finally:
+        vip.set_bilateral_frames_in_flight(0)
+    fn = oracle.bilateral if c["kind"] == "bilateral" else oracle.adaptive
+    for f, x in enumerate(imgs):
+        want = fn(x, c["k"], c["ss"], c["sc"], profile=c["profile"])[c["row0"]:c["row0"] + c["out_rows"]]
+        got = dev.get(dsts[f])
+        d = np.argwhere(got != want)
+        assert not len(d), f"{c} frame {f}: {len(d)} mismatches, first {d[:3].tolist()}"
