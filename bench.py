@@ -682,19 +682,23 @@ def rccl_evidence(shards, rank, world, expected_count) -> dict:
     import torch.distributed as dist
 
     from various_image_processings_amd.sharded import rccl_version
-    infos = [s.comm_info() for s in shards]
-    mine = dict(rank=rank, count=infos[0]["count"], user_rank=infos[0]["user_rank"], device=infos[0]["device"],
-                pci_bus_id=infos[0]["pci_bus_id"], shards=len(infos),
-                shards_agree=all((i["count"], i["user_rank"], i["device"]) ==
-                                 (infos[0]["count"], infos[0]["user_rank"], infos[0]["device"]) for i in infos))
+    try:
+        infos = [s.comm_info() for s in shards]
+        mine = dict(rank=rank, count=infos[0]["count"], user_rank=infos[0]["user_rank"], device=infos[0]["device"],
+                    pci_bus_id=infos[0]["pci_bus_id"], shards=len(infos),
+                    shards_agree=all((i["count"], i["user_rank"], i["device"]) ==
+                                     (infos[0]["count"], infos[0]["user_rank"], infos[0]["device"]) for i in infos))
+    except Exception as e:  # every rank still reaches the gather (a raise here would hang the peers)
+        mine = dict(rank=rank, count=None, user_rank=None, device=None, pci_bus_id=f"unknown (rank {rank})",
+                    shards=len(shards), shards_agree=False, error=repr(e))
     ranks = [None] * world
     if world > 1:
         dist.all_gather_object(ranks, mine)
     else:
         ranks = [mine]
-    counts = sorted({r_["count"] for r_ in ranks})
+    counts = sorted({r_["count"] for r_ in ranks}, key=lambda c: (c is None, c or 0))
     buses = [r_["pci_bus_id"] for r_ in ranks]
-    problems = []
+    problems = [f"rank {r_['rank']}: comm_info failed: {r_['error']}" for r_ in ranks if r_.get("error")]
     if counts != [expected_count]:
         problems.append(f"communicator sizes {counts}, expected {expected_count}")
     if expected_count > 1 and any(r_["user_rank"] != r_["rank"] for r_ in ranks):

@@ -1,8 +1,12 @@
 """TEST INFRASTRUCTURE ONLY: ctypes wrapper of oracle/liboracle.so (vip_oracle.c).
 
-Parity status: "parity unpinned" against reference execution (the reference's
-include/cpp and src/ need OpenCV / nvcc, absent here); the mt19937 input
-generator is pinned to the reference's own test/random_array.hpp (tests/golden).
+Parity status: pinned where the reference ships an executable oracle. The REF
+profile equals the reference tests' own CPU oracles (test/adaptive_bilateral_filter.cu,
+test/bilateral_texture_filter.cu, test/gradient.cu Ref* code, compiled in place by
+oracle/Makefile) bit for bit on tests/golden/ref_oracles.npz: adaptive, gradient,
+blur/mRTV and guide are pinned. Bilateral / joint bilateral stay "parity unpinned":
+their only reference oracle is cv::bilateralFilter (OpenCV, absent here). The
+mt19937 input generator is pinned to test/random_array.hpp (tests/golden).
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may use this.
 """
 from __future__ import annotations
@@ -18,6 +22,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 CUDA = 0  # src/<filter>_impl.cu numerics (float LUT coefficients, fma accumulate)
 CPP = 1   # include/cpp numerics (double LUT coefficients, mul + add)
+REF = 2   # the reference tests' own CPU oracles (test/*.cu Ref*: float LUT, mul + add, expf)
 
 _lib = None
 

@@ -22,6 +22,13 @@
  *   VIPO_CPP  (1): include/cpp/<filter>.hpp — double-coefficient LUTs
  *                  (bilateral_filter.hpp:15-16), separate multiply and add
  *                  (x86-64 baseline, no FMA), float epsilon in mRTV.
+ *   VIPO_REF  (2): the reference TESTS' own CPU oracles (test/adaptive_bilateral_filter.cu:7-119,
+ *                  test/bilateral_texture_filter.cu:8-113, test/gradient.cu:9-34): float-coefficient
+ *                  LUTs as CUDA, separate multiply and add as CPP (host code, no FMA), float
+ *                  epsilon / FLT_MAX seed / unfused blend and glibc expf in the texture stages, and
+ *                  the gradient's f32 order sum_c h*h then sum_c v*v, unfused. The oracle's REF
+ *                  outputs equal those oracles compiled from the reference (oracle/Makefile ->
+ *                  oracle/_ref/libref_test_oracles.so) bit for bit on tests/golden/ref_oracles.npz.
  * Build with -ffp-contract=off so gcc never fuses what the reference does not.
  */
 #include <math.h>
@@ -29,7 +36,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { VIPO_CUDA = 0, VIPO_CPP = 1 };
+enum { VIPO_CUDA = 0, VIPO_CPP = 1, VIPO_REF = 2 };
 
 /* Numerics-sensitivity variants of the CUDA profile (tests/test_oracle.py,
  * scripts/numerics_sensitivity.py). Each bit replaces one code-generation choice
@@ -129,9 +136,9 @@ void vipo_color_lut(int len, float sigma_color, int profile, float* out) {
         out[i] = profile == VIPO_CPP ? (float)exp((double)(i * i) * cd) : expf((float)(i * i) * cf);
 }
 
-/* accumulate one tap: CUDA contracts `sum += p * w` into fmaf; CPP does not. */
+/* accumulate one tap: CUDA contracts `sum += p * w` into fmaf; CPP and REF do not. */
 #define ACC(profile, sum, p, w) \
-    ((profile) == VIPO_CPP ? ((sum) + (float)(p) * (w)) : fmaf((float)(p), (w), (sum)))
+    ((profile) != VIPO_CUDA ? ((sum) + (float)(p) * (w)) : fmaf((float)(p), (w), (sum)))
 
 /* ------------------------------------------------------------------------- */
 /* Bilateral / joint bilateral.                                               */
@@ -161,7 +168,7 @@ static void bilateral_rows(const uint8_t* src, const uint8_t* guide, uint8_t* ds
                     s0 = ACC(profile, s0, p[0], w);
                     s1 = ACC(profile, s1, p[1], w);
                     s2 = ACC(profile, s2, p[2], w);
-                    if (profile != VIPO_CPP && (g_variant & VIPO_V_SUMK_FMA))
+                    if (profile == VIPO_CUDA && (g_variant & VIPO_V_SUMK_FMA))
                         sk = fmaf(space[(ky + radius) * ksize + (kx + radius)], color[d], sk);
                     else
                         sk = sk + w;
@@ -236,7 +243,7 @@ void vipo_adaptive_rows(const uint8_t* src, uint8_t* dst, int width, int height,
                     s0 = ACC(profile, s0, p[0], w);
                     s1 = ACC(profile, s1, p[1], w);
                     s2 = ACC(profile, s2, p[2], w);
-                    if (profile != VIPO_CPP && (g_variant & VIPO_V_SUMK_FMA))
+                    if (profile == VIPO_CUDA && (g_variant & VIPO_V_SUMK_FMA))
                         sk = fmaf(space[(ky + radius) * ksize + (kx + radius)], color[(int)dist], sk);
                     else
                         sk = sk + w;
@@ -282,7 +289,7 @@ static void gradient_impl(const void* src, int is_f32, float* dst, int width, in
                     dy = dy + (float)(v * v);
                 }
                 out = sqrtf(dx + dy);
-            } else if (profile == VIPO_CPP) {
+            } else if (profile == VIPO_CPP) {  /* include/cpp/gradient.hpp */
                 float sum = 0.f;
                 for (int c = 0; c < ch; c++) {
                     const float h = PIX(xp, y, c) - PIX(xm, y, c);
@@ -290,6 +297,17 @@ static void gradient_impl(const void* src, int is_f32, float* dst, int width, in
                     sum += h * h + v * v;
                 }
                 out = sqrtf(sum);
+            } else if (profile == VIPO_REF) {  /* test/gradient.cu:11-31: unfused, h then v */
+                float dx = 0.f, dy = 0.f;
+                for (int c = 0; c < ch; c++) {
+                    const float h = PIX(xm, y, c) - PIX(xp, y, c);
+                    dx = dx + h * h;
+                }
+                for (int c = 0; c < ch; c++) {
+                    const float v = PIX(x, ym, c) - PIX(x, yp, c);
+                    dy = dy + v * v;
+                }
+                out = sqrtf(dx + dy);
             } else {
                 float dx = 0.f, dy = 0.f;
                 for (int c = 0; c < ch; c++) {
@@ -347,7 +365,7 @@ void vipo_blur_rtv(const uint8_t* img, const float* mag, float* blurred, float* 
             float* b = blurred + ((size_t)y * width + x) * 3;
             b[0] = s0 / kk; b[1] = s1 / kk; b[2] = s2 / kk;
             const float num = (imax - imin) * mmax;
-            rtv[(size_t)y * width + x] = profile == VIPO_CPP ? num / (msum + 1e-9f)
+            rtv[(size_t)y * width + x] = profile != VIPO_CUDA ? num / (msum + 1e-9f)
                                                              : (float)((double)num / ((double)msum + 1e-9));
         }
     }
@@ -370,7 +388,7 @@ void vipo_guide(const float* blurred, const float* rtv, uint8_t* guide, int widt
     const float sigma_alpha = 1.f / (float)(5 * ksize);
     for (int y = 0; y < height; y++) {
         for (int x = 0; x < width; x++) {
-            float rmin = profile == VIPO_CPP ? 3.402823466e+38f : 1e10f;
+            float rmin = profile != VIPO_CUDA ? 3.402823466e+38f : 1e10f;
             int mx = 0, my = 0;
             for (int ky = -radius; ky <= radius; ky++) {
                 const int yc = clampi(y + ky, 0, height - 1);
@@ -381,9 +399,9 @@ void vipo_guide(const float* blurred, const float* rtv, uint8_t* guide, int widt
                 }
             }
             const float arg = sigma_alpha * (rtv[(size_t)y * width + x] - rtv[(size_t)my * width + mx]);
-            float e = (float)exp((double)arg);
-            if (profile != VIPO_CPP && (g_variant & VIPO_V_EXP_UP)) e = nextafterf(e, INFINITY);
-            if (profile != VIPO_CPP && (g_variant & VIPO_V_EXP_DOWN)) e = nextafterf(e, 0.f);
+            float e = profile == VIPO_REF ? expf(arg) : (float)exp((double)arg); /* REF: std::exp(float) */
+            if (profile == VIPO_CUDA && (g_variant & VIPO_V_EXP_UP)) e = nextafterf(e, INFINITY);
+            if (profile == VIPO_CUDA && (g_variant & VIPO_V_EXP_DOWN)) e = nextafterf(e, 0.f);
             const float alpha = 2.f / (1.f + e) - 1.f;
             const float beta = 1.f - alpha;
             const float* bm = blurred + ((size_t)my * width + mx) * 3;
@@ -391,7 +409,7 @@ void vipo_guide(const float* blurred, const float* rtv, uint8_t* guide, int widt
             uint8_t* g = guide + ((size_t)y * width + x) * 3;
             for (int c = 0; c < 3; c++) {
                 float v;
-                if (profile == VIPO_CPP || (g_variant & VIPO_V_BLEND_NO)) v = alpha * bm[c] + beta * bc[c] + 0.5f;
+                if (profile != VIPO_CUDA || (g_variant & VIPO_V_BLEND_NO)) v = alpha * bm[c] + beta * bc[c] + 0.5f;
                 else if (g_variant & VIPO_V_BLEND_B) v = fmaf(beta, bc[c], alpha * bm[c]) + 0.5f;
                 else v = fmaf(alpha, bm[c], beta * bc[c]) + 0.5f;
                 g[c] = (uint8_t)clampi((int)v, 0, 255);

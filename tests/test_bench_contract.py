@@ -261,6 +261,12 @@ def test_rccl_evidence_flags_what_is_not_an_n_gpu_run(monkeypatch):
     mixed = bench.rccl_evidence([_FakeShard(1, 0, 0, "b"), _FakeShard(2, 0, 0, "b")], 0, 1, 1)
     assert any("disagree" in p for p in mixed["problems"])
 
+    class _Broken:
+        def comm_info(self):
+            raise RuntimeError("ncclCommCount failed")
+    broken = bench.rccl_evidence([_Broken()], 0, 1, 1)  # no raise: the peers must reach the gather
+    assert any("comm_info failed" in p for p in broken["problems"])
+
 
 def test_launched_prefers_the_multi_frame_form():
     """A shared launch's kernel (`..._frames_kernel<`) names the line's kernel when present;

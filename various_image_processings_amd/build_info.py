@@ -60,4 +60,4 @@ def check() -> dict:
     libs_now = {n: _lib_sha(n) for n in LIBS}
     return dict(built_utc=info.get("built_utc"), compiler=info.get("compiler"),
                 sources_sha256=now_src[:16], sources_match=now_src == info.get("sources_sha256"),
-                libs_match=all(libs_now[n] == info["libs"].get(n) for n in LIBS))
+                libs_match=all(libs_now[n] is not None and libs_now[n] == info.get("libs", {}).get(n) for n in LIBS))
