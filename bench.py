@@ -54,6 +54,9 @@ sys.path.insert(0, ROOT)
 PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector (== f32 MFMA) peak
 VALU_SIMDS = 1024            # 256 CUs x 4 SIMDs
+# how the N = 1 roofline's launch durations are measured (bench.measure)
+LAUNCH_TIMING = ("vip_kernel_timing: hipExtLaunchKernel events stamped with each kernel's own begin and end, "
+                 "max(4, K/4) frames back to back on one stream after the timed region")
 VALU_CYCLES_PER_INSTR = 2    # a wave64 VALU instruction issues over 2 cycles (MI355X_MICROARCH.md)
 NBUF = 12
 
@@ -487,7 +490,7 @@ def valu_issue(config: str, kernel, launch_ms: float):
 
 def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms, kernels: list) -> dict:
     """C4: the dominant kernel of the iteration (the larger of the fused guide stage and
-    the joint bilateral, live event-timed per launch) with its own roof, the other one
+    the joint bilateral, each launch's own duration from vip_kernel_timing) with its own roof, the other one
     beside it, and the pipeline's HBM rate from the bytes the kernels actually move
     (committed PMC summary, per frame) -- not the unfused stage-wise decomposition."""
     nitr, k = cfg["nitr"], cfg["ksize"]
@@ -527,9 +530,7 @@ def texture_roofline(config: str, cfg: dict, px: int, frame_ms: float, stage_ms,
                        frac=guide["hbm"]["frac"], traffic=guide["hbm"]["traffic"], traffic_source=guide["hbm"]["traffic_source"],
                        traffic_algorithmic=6.0 * px)
         out.update(kernel=dom["kernel"], avg_launch_ms=dom["avg_launch_ms"], dominant=dom, other=other,
-                   stage_split=dict(method="timed-region frame time split by the guide:JBF ratio of evented frames",
-                                    guide_evented_ms=round(stage_ms["guide_evented"], 4),
-                                    jbf_evented_ms=round(stage_ms["jbf_evented"], 4)))
+                   launch_timing=LAUNCH_TIMING)
     traffic, tsrc = pmc_traffic(config, [guide_k, jbf_k], nitr)
     pipe = dict(frame_ms=round(frame_ms, 4), launches=2 * nitr, traffic_per_frame=traffic, traffic_source=tsrc)
     if traffic:
@@ -746,17 +747,10 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
                 t_.set_mode(_TextureImpl.FUSED)
         srcs = make_frames(torch, args.data, rows, w, dev, gen, NBUF)
         dsts = [torch.empty((rows, w, 3), dtype=torch.uint8, device=dev) for _ in range(NBUF)]
-        smarks = []
         sp, dp = [t.data_ptr() for t in srcs], [t.data_ptr() for t in dsts]
 
         def run(i, s=stream, h=0):  # s is streams[h]; raw addresses keep host work per launch small
             texs[h].execute(sp[i % NBUF], dp[i % NBUF], stream=sraw[h])
-
-        def run_staged(i):
-            """one frame with per-stage events (vip_texture_run_timed)"""
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * cfg["nitr"] + 1)]
-            texs[0].execute_timed(srcs[i % NBUF], dsts[i % NBUF], ev, stream=stream)
-            smarks.append(ev)
     else:
         shards = None
         if multi and args.exchange == "native":
@@ -1077,17 +1071,22 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
             kernel_ms = parts["kernel_ms"]
     else:
         kernel_ms = ev0.elapsed_time(ev1) / args.steps
-        if S_run > 1 or B > 1:
-            # the roofline is per kernel: its launch duration comes from max(4, K/4) more
-            # frames (a multiple of B) on ONE stream, back to back, after the timed region
-            # (the S-stream launches overlap, so their event spans are not launch durations;
-            # with B > 1 one launch carries B frames and the duration is per frame)
-            n1 = max(4, args.steps // 4)
-            n1 += (-n1) % B
-            timed_kernels = set(res["kernels_timed"])
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # The roofline is per kernel: its launch durations come from max(4, K/4) more frames
+        # (a multiple of B) on ONE stream, back to back, after the timed region, each launch
+        # carrying events the runtime stamps with the kernel's own begin and end
+        # (vip_kernel_timing, hipExtLaunchKernel: no marker packet in the stream, so these
+        # are the durations rocprofv3 --kernel-trace reports). The S-stream launches of the
+        # timed region overlap each other, so their spans are not kernel durations; with
+        # B > 1 one launch carries B frames and the duration is divided by B.
+        import various_image_processings_amd as vip_
+        n1 = max(4, args.steps // 4)
+        n1 += (-n1) % B
+        timed_kernels = set(res["kernels_timed"])
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        per_frame = 2 * cfg["nitr"] if cfg["kind"] == "texture" else 1
 
-            def one_stream(first):
+        def one_stream(first):
+            with vip_.kernel_timing(n1 * per_frame) as kt:
                 e0.record(stream)
                 if B > 1:
                     for j in range(first, first + n1, B):
@@ -1097,28 +1096,31 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
                     for i in range(n1):
                         run(first + i)
                 e1.record(stream)
-                torch.cuda.synchronize(dev)
-                return e0.elapsed_time(e1) / n1
+            torch.cuda.synchronize(dev)
+            return e0.elapsed_time(e1) / n1, kt.durations()
 
-            single_ms = one_stream(after + (-after) % B)
+        single_ms, kdur = one_stream(after + (-after) % B)
+        if not set(launched_kernels()) <= timed_kernels:
+            # one stream made the library pick another tiling than the frames in flight
+            # did (its small-frame tiling counts the streams in use): time the timed
+            # region's kernel, back to back on one stream, with the frame count forced
+            # to the S the timed frames had (vip_bilateral_set_frames_in_flight)
+            vip_.set_bilateral_frames_in_flight(min(S_run, 4))
+            try:
+                single_ms, kdur = one_stream(after + n1 + (-(after + n1)) % B)
+            finally:  # back to the run's own setting (--frames-in-flight, else counted)
+                vip_.set_bilateral_frames_in_flight(args.frames_in_flight)
+            res["launch_timing"] = (f"one stream, the tiling planned for the timed region's {S_run} frames in "
+                                    f"flight (vip_bilateral_set_frames_in_flight)")
             if not set(launched_kernels()) <= timed_kernels:
-                # one stream made the library pick another tiling than the frames in flight
-                # did (its small-frame tiling counts the streams in use): time the timed
-                # region's kernel, back to back on one stream, with the frame count forced
-                # to the S the timed frames had (vip_bilateral_set_frames_in_flight)
-                import various_image_processings_amd as vip_
-                vip_.set_bilateral_frames_in_flight(min(S_run, 4))
-                try:
-                    single_ms = one_stream(after + n1 + (-(after + n1)) % B)
-                finally:  # back to the run's own setting (--frames-in-flight, else counted)
-                    vip_.set_bilateral_frames_in_flight(args.frames_in_flight)
-                res["launch_timing"] = (f"one stream, the tiling planned for the timed region's {S_run} frames in "
-                                        f"flight (vip_bilateral_set_frames_in_flight)")
-                if not set(launched_kernels()) <= timed_kernels:
-                    res["launch_timing"] += "; WARNING: another kernel ran"
-            if B > 1:
-                res["launch_timing"] = (res.get("launch_timing", "one stream") +
-                                        f"; {B} frames per launch, duration per frame")
+                res["launch_timing"] += "; WARNING: another kernel ran"
+        if B > 1:
+            res["launch_timing"] = (res.get("launch_timing", "one stream") +
+                                    f"; {B} frames per launch, duration per frame")
+        # per kernel: launches, mean / min / max duration (ms, per launch)
+        res["kernel_durations"] = {n: dict(launches=len(v), mean_ms=sum(v) / len(v), min_ms=min(v), max_ms=max(v))
+                                   for n, v in kdur.items()}
+        res["span_one_stream_ms"] = single_ms  # per frame, launch gaps included
     launch_ms = single_ms if single_ms is not None else kernel_ms
     # one frame's latency: the whole launch that carries it on an idle stream (N = 1) or
     # its RCCL group's exchange and launches (N > 1); the reference's public call blocks for
@@ -1129,20 +1131,12 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         res["frame_latency_ms"] = parts.get("group_latency_ms", parts.get("run_ms", kernel_ms))
     fused = cfg["kind"] == "texture" and world == 1 and not args.loopback and args.texture_mode == "fused"
     if cfg["kind"] == "texture" and world == 1 and not args.loopback and not fused:
-        # Per-stage split of the frame: an event between two launches costs a few us of
-        # stream time (measured: +4 us on each stage against rocprofv3), so the timed
-        # frames above carry no inner events; max(4, K/4) further frames, after the
-        # timed region, record events around every launch, and their guide : JBF ratio
-        # splits the clean frame time of the timed region (stage_ms, per launch).
-        for i in range(max(4, args.steps // 4)):
-            run_staged(after + i)
-        torch.cuda.synchronize(dev)
-        nit = cfg["nitr"]
-        guide = sum(m[2 * t].elapsed_time(m[2 * t + 1]) for m in smarks for t in range(nit))
-        jbf = sum(m[2 * t + 1].elapsed_time(m[2 * t + 2]) for m in smarks for t in range(nit))
-        per = launch_ms / nit
-        res["stage_ms"] = {"guide": per * guide / (guide + jbf), "jbf": per * jbf / (guide + jbf),
-                           "guide_evented": guide / (len(smarks) * nit), "jbf_evented": jbf / (len(smarks) * nit)}
+        # per-stage kernel durations (vip_kernel_timing), per launch
+        kd = res["kernel_durations"]
+        g_ = [v["mean_ms"] for n, v in kd.items() if n.startswith("void vip::texture_guide_fused_kernel")]
+        j_ = [v["mean_ms"] for n, v in kd.items() if n.startswith(f"void vip::bilateral_kernel<{k - 1},")]
+        if g_ and j_:
+            res["stage_ms"] = {"guide": g_[0], "jbf": j_[0]}
     keys = ["elapsed", "launch", "host", "latency"] + (sorted(parts) if parts else [])
     vals = [elapsed, launch_ms, host_s, res.get("frame_latency_ms", 0.0)] + \
         ([parts[x] for x in sorted(parts)] if parts else [])
@@ -1274,27 +1268,32 @@ def main():
     else:
         taps = circle_taps(r)
         flops = FLOP_PER_TAP[cfg["kind"]] * taps * px_per_rank
-        tflops = flops / (launch_ms * 1e-3) / 1e12
-        hbm = 6.0 * px_per_rank / (launch_ms * 1e-3) / 1e9
-        # the committed PMC summaries are single-GPU whole-frame launches
         # the exact instantiation this run launched (vip_launched_kernels), for the PMC lookup
         kname = launched(m["kernels"], cfg.get("kernel", f"void vip::{cfg['kind']}_kernel<{r},"))
         # a shared launch (vip_*_run_rows_batch, B > 1) carries B frames: durations, PMC
         # counts and bytes are per frame (the summaries record the frames per dispatch
         # they were profiled with)
         fpl = m["batch"] if kname and "_frames_kernel<" in kname else 1
+        # N = 1: the kernel's own begin-to-end duration per frame (vip_kernel_timing); N > 1:
+        # the per-rank device time of one step (exchange included, below)
+        kd = (m.get("kernel_durations") or {}).get(kname)
+        dur_ms = kd["mean_ms"] / fpl if kd else launch_ms
+        tflops = flops / (dur_ms * 1e-3) / 1e12
+        hbm = 6.0 * px_per_rank / (dur_ms * 1e-3) / 1e9
         traffic, tsrc = (None, None) if sharded else pmc_traffic(args.config, [kname])
         roof = dict(bound="valu-fp32", achieved=round(tflops, 3), peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
                     frac=round(tflops / PEAK_FP32_TFLOPS, 4), traffic=traffic, traffic_source=tsrc,
                     traffic_algorithmic=6.0 * px_per_rank,
                     kernel=cfg.get("kernel_label", f"{cfg['kind']}_kernel<R={r}>"), kernel_name=kname,
-                    avg_launch_ms=round(launch_ms, 4),
+                    avg_launch_ms=round(dur_ms, 4),
+                    **({"launch_timing": LAUNCH_TIMING, "launches_timed": kd["launches"],
+                        "span_one_stream_ms": round(m["span_one_stream_ms"], 4)} if kd else {}),
                     flop_per_px=FLOP_PER_TAP[cfg["kind"]] * taps, in_support_taps=taps,
-                    gtaps_per_s=round(taps * px_per_rank / (launch_ms * 1e-3) / 1e9, 1),
+                    gtaps_per_s=round(taps * px_per_rank / (dur_ms * 1e-3) / 1e9, 1),
                     hbm=dict(achieved=round(hbm, 2), peak=PEAK_HBM_GBS, unit="GB/s", frac=round(hbm / PEAK_HBM_GBS, 5),
                              bytes_per_px=6))
         if not sharded:  # the committed PMC summaries are whole-frame launches
-            roof["valu_issue"] = valu_issue(args.config, kname, launch_ms)
+            roof["valu_issue"] = valu_issue(args.config, kname, dur_ms)
             if fpl > 1:
                 roof["frames_per_launch"] = fpl
             roof["isolated_sample"] = isolated_sample(args.config, kname)

@@ -47,6 +47,18 @@ int vip_abi_version(void);
  * length. Returns the full length. No reference counterpart: it lets a benchmark
  * name the exact template instantiation it timed. */
 int vip_launched_kernels(char* buf, size_t len);
+/* Kernel-duration recorder of the calling thread (measurement; no reference counterpart).
+ * After vip_kernel_timing_begin(capacity) the next `capacity` kernels this thread launches
+ * through the library carry a (start, stop) event pair that the runtime stamps with the
+ * kernel's own begin and end (hipExtLaunchKernel): no marker packet enters the stream, so a
+ * duration is what rocprofv3 --kernel-trace reports for that launch. Begin clears earlier
+ * records (capacity 1..65536). vip_kernel_timing_end() stops recording and returns the
+ * number of launches recorded. vip_kernel_timing_get(i, &ms, name, len), after end, waits
+ * for launch i to finish and returns its duration and (if name) its kernel name as
+ * vip_launched_kernels names it. */
+int vip_kernel_timing_begin(int capacity);
+int vip_kernel_timing_end(void);
+int vip_kernel_timing_get(int index, float* ms, char* name, size_t len);
 const char* vip_error_string(int code);
 /* Largest filter radius (ksize/2) any filter accepts (32: bilateral ksize 65). */
 int vip_max_radius(void);

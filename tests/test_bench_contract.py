@@ -117,6 +117,44 @@ def test_committed_lines_time_the_roofline_on_one_stream():
         assert abs(iso / 1e3 - launch_ms) / launch_ms < 0.03, (cfg, iso, launch_ms)
 
 
+def roofline_duration_fits_a_step(line) -> bool:
+    """The kernel duration behind `roofline.frac` (avg_launch_ms, per frame) fits in the
+    measured step: <= ms_per_step x frames per launch. It holds for
+    kernels that fill the chip (C2, C3, C5, C4's stages); C1's 512^2 launches each hold a
+    fraction of the CUs and run side by side, which `roofline.in_flight` reports."""
+    r = line["roofline"]
+    fpl = r.get("frames_per_launch", 1)
+    if "dominant" in r:  # C4: a stage launch against the frame's step (10 launches per frame)
+        return r["avg_launch_ms"] <= line["ms_per_step"]
+    return r["avg_launch_ms"] <= line["ms_per_step"] * fpl
+
+
+def test_roofline_duration_rule():
+    ok = dict(ms_per_step=0.176, roofline=dict(avg_launch_ms=0.1705))
+    stale = dict(ms_per_step=0.176, roofline=dict(avg_launch_ms=0.1821))  # BENCH_r05's span
+    assert roofline_duration_fits_a_step(ok) and not roofline_duration_fits_a_step(stale)
+
+
+def test_committed_lines_divide_by_a_kernel_duration_that_fits_a_step():
+    """Every committed N = 1 line timed with vip_kernel_timing (kernel-stamped events) of a
+    chip-filling config: the duration behind frac fits in ms_per_step."""
+    import glob
+    lines = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_c[2345]_bench.json"))) + \
+            sorted(glob.glob(os.path.join(ROOT, "BENCH_r*.json"))):
+        try:
+            line = json.load(open(f))
+        except ValueError:
+            continue
+        line = line.get("parsed", line)
+        if isinstance(line, dict) and line.get("n_gpus") == 1 and "launch_timing" in line.get("roofline", {}):
+            lines.append((f, line))
+    if not lines:
+        pytest.skip("no committed line timed with vip_kernel_timing yet")
+    for f, line in lines:
+        assert roofline_duration_fits_a_step(line), (f, line["roofline"]["avg_launch_ms"], line["ms_per_step"])
+
+
 def test_halo_batches_keep_buffers_on_one_stream():
     """bench.py N > 1 native path: frame i in batch i // B on stream (i // B) % S. For
     every batch size it may choose, each buffer (i % NBUF) always meets the same stream,

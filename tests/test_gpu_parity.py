@@ -602,6 +602,31 @@ def test_launched_kernels_names_the_instantiation(dev, oracle):
     assert all("(" not in n for n in names)
 
 
+def test_kernel_timing_stamps_each_launch(dev, oracle):
+    """vip_kernel_timing: each launch inside the window carries kernel-stamped events (its
+    own begin and end, hipExtLaunchKernel); launches beyond the capacity run plainly; the
+    outputs are the same as without the recorder."""
+    img = oracle.random_image(640, 360)
+    d = dev.empty((360, 640, 3))
+    f = vip.CudaBilateralFilter(640, 360, 15)
+    with vip.kernel_timing(3) as kt:
+        for _ in range(5):
+            f.bilateral_filter(dev.put(img), d)
+    assert kt.count == 3
+    rec = kt.records()
+    assert all(n.startswith("void vip::bilateral_kernel<7,") for n, _ in rec)
+    assert all(0.0 < ms < 100.0 for _, ms in rec)
+    assert np.array_equal(dev.get(d), oracle.bilateral(img, 15, threads=16))
+    t = _TextureImpl(300, 200, 5, 2)
+    with vip.kernel_timing(16) as kt:
+        t.execute(dev.put(img[:200, :300].copy()), dev.empty((200, 300, 3)))
+    dur = kt.durations()
+    assert kt.count == 4 and sum(len(v) for v in dur.values()) == 4
+    assert any(n.startswith("void vip::texture_guide_fused_kernel<2, false>") for n in dur)
+    with pytest.raises(vip.VipError):
+        vip.kernel_timing(0).__enter__()
+
+
 def test_small_frame_tiling_follows_frames_in_flight(dev, oracle):
     """The plain kernel's small-frame tiling counts the frames in flight (distinct streams
     among the device's last 8 launches): lenna-sized 512^2 frames on 4 streams take the

@@ -25,6 +25,7 @@ from .filters import (  # noqa: F401
     DeviceImage,
     cuda_gradient,
     device_synchronize,
+    kernel_timing,
     launched_kernels,
     max_ksize,
     set_bilateral_frames_in_flight,

@@ -31,6 +31,9 @@ _c_size_t = ctypes.c_size_t
 SIGNATURES = {
     "vip_abi_version": (_c_int, []),
     "vip_launched_kernels": (_c_int, [ctypes.c_char_p, _c_size_t]),
+    "vip_kernel_timing_begin": (_c_int, [_c_int]),
+    "vip_kernel_timing_end": (_c_int, []),
+    "vip_kernel_timing_get": (_c_int, [_c_int, ctypes.POINTER(_c_float), ctypes.c_char_p, _c_size_t]),
     "vip_error_string": (ctypes.c_char_p, [_c_int]),
     "vip_max_radius": (_c_int, []),
     "vip_max_ksize": (_c_int, [_c_int]),

@@ -355,11 +355,13 @@ static int launch_adaptive_ne(const StencilArgs& a, hipStream_t stream) {
     args.tiles_total = args.tiles_frame * (multi ? a.nframes : 1);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
+    args.tail_full = args.tiles_total;  // no cut: every item a whole tile on the XCD map
+    args.tail_shift = 0;
     // the last round in pieces (C3 slab at 8 GPUs, 6 frames per launch, 8 CUs free: one
     // stream 0.0500 -> 0.0477 ms per frame, two streams 0.0429-0.0430 both ways; at 4 GPUs
     // on two streams 0.0960 -> 0.0939; profiles/r05_slab_batch_ab{,2}.txt)
     if (multi) plan_tail(args, blocks, WAVES);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
+    launch(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }
 

@@ -407,13 +407,15 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     args.tiles_total = args.tiles_frame * (multi ? a.nframes : 1);
     if (args.tiles_total == 0) return 0;
     const int blocks = persistent_blocks(args.tiles_total, a.free_cus);
+    args.tail_full = args.tiles_total;  // no cut: every item a whole tile on the XCD map
+    args.tail_shift = 0;
     // the last round in pieces for one frame in flight only: with two streams the other
     // stream's launch already fills the CUs a whole-tile last round leaves idle, and the
     // pieces' fewer waves per CU cost more CU time (C2 slab at 8 GPUs, 6 frames per launch,
     // 8 CUs free: one stream 0.0256-0.0258 -> 0.0250 ms per frame, two streams 0.0222-0.0225
     // -> 0.0231-0.0233; profiles/r05_slab_batch_ab{,2}.txt)
     if (multi && a.inflight <= 1) plan_tail(args, blocks, WAVES);
-    hipLaunchKernelGGL(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
+    launch(kern, dim3(blocks), dim3(WAVES * 64), LDS, stream, args);
     return (int)hipGetLastError();
 }
 

@@ -15,6 +15,7 @@
 #include <dlfcn.h>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "vip_stencil.hpp"
 
@@ -161,7 +162,7 @@ static void fill_args(StencilArgs& a, int width, const uint8_t* src, size_t src_
     a.nframes = 1;
     a.tiles_frame = 0;
     a.free_cus = 0;
-    a.tail_full = 0;
+    a.tail_full = 0;  // set per launch (launch_*_ne: tiles_total, or plan_tail)
     a.tail_shift = 0;
     for (int f = 0; f < kMaxBatchFrames; ++f) {
         a.fsrc[f] = src;
@@ -280,6 +281,36 @@ static RtArgs rt_args(const RtTables& t, int radius, int width, const uint8_t* s
 namespace {
 thread_local const void* g_launched[16];  // distinct kernels launched since the last query
 thread_local int g_nlaunched = 0;
+
+// vip_kernel_timing_*: a per-thread pool of event pairs on one device, the kernel of each
+// recorded launch, and how many of the `cap` slots are used
+struct KernelTiming {
+    std::vector<hipEvent_t> ev;  // 2 per slot: start, stop
+    std::vector<const void*> kern;
+    int device = -1, cap = 0, n = 0;
+    bool on = false;
+    ~KernelTiming() {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+};
+thread_local KernelTiming g_timing;
+
+// The profiler's name of a kernel handle: the exported symbol's mangled name (dladdr; the
+// runtime's lookup is the fallback), demangled, without the parameter list.
+std::string kernel_name(const void* kern) {
+    Dl_info info{};
+    const char* mangled = dladdr(kern, &info) && info.dli_sname && info.dli_saddr == kern
+                              ? info.dli_sname
+                              : hipKernelNameRefByPtr(kern, nullptr);
+    if (!mangled) return {};
+    int st = 0;
+    char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
+    std::string name = st == 0 && dem ? dem : mangled;
+    std::free(dem);
+    const size_t paren = name.find('(');
+    if (paren != std::string::npos) name.resize(paren);  // the profiler summaries' key: no parameter list
+    return name;
+}
 }  // namespace
 
 namespace vip {
@@ -288,6 +319,14 @@ void note_launch(const void* kern) {
         if (g_launched[i] == kern) return;
     if (g_nlaunched < 16) g_launched[g_nlaunched++] = kern;
 }
+
+LaunchEvents timing_events(const void* kern) {
+    KernelTiming& t = g_timing;
+    if (!t.on || t.n >= t.cap) return {nullptr, nullptr};
+    t.kern[t.n] = kern;
+    const int i = t.n++;
+    return {t.ev[2 * i], t.ev[2 * i + 1]};
+}
 }  // namespace vip
 
 extern "C" {
@@ -295,20 +334,8 @@ extern "C" {
 int vip_launched_kernels(char* buf, size_t len) {
     std::string all;
     for (int i = 0; i < g_nlaunched; ++i) {
-        // the kernel handle is an exported symbol of this library: its name is the kernel's
-        // mangled name (dladdr); the runtime's lookup is the fallback (some runtimes return null)
-        Dl_info info{};
-        const char* mangled = dladdr(g_launched[i], &info) && info.dli_sname && info.dli_saddr == g_launched[i]
-                                  ? info.dli_sname
-                                  : hipKernelNameRefByPtr(g_launched[i], nullptr);
-        if (!mangled) continue;
-        int st = 0;
-        char* dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &st);
-        std::string name = st == 0 && dem ? dem : mangled;
-        std::free(dem);
-        const size_t paren = name.find('(');
-        if (paren != std::string::npos) name.resize(paren);  // the profiler summaries' key: no parameter list
-        all += (all.empty() ? "" : "\n") + name;
+        const std::string name = kernel_name(g_launched[i]);
+        if (!name.empty()) all += (all.empty() ? "" : "\n") + name;
     }
     if (buf && len) {
         g_nlaunched = 0;  // a size query (no buffer) keeps the list
@@ -317,6 +344,47 @@ int vip_launched_kernels(char* buf, size_t len) {
         buf[n] = 0;
     }
     return (int)all.size();
+}
+
+int vip_kernel_timing_begin(int capacity) {
+    if (capacity < 1 || capacity > (1 << 16)) return VIP_ERR_INVALID_ARGUMENT;
+    KernelTiming& t = g_timing;
+    int dev = 0;
+    VIP_HIP_CHECK(hipGetDevice(&dev));
+    if (dev != t.device) {  // events belong to the device current at their creation
+        for (hipEvent_t e : t.ev) (void)hipEventDestroy(e);
+        t.ev.clear();
+        t.device = dev;
+    }
+    while ((int)t.ev.size() < 2 * capacity) {
+        hipEvent_t e = nullptr;
+        VIP_HIP_CHECK(hipEventCreate(&e));
+        t.ev.push_back(e);
+    }
+    t.kern.assign((size_t)capacity, nullptr);
+    t.cap = capacity;
+    t.n = 0;
+    t.on = true;
+    return 0;
+}
+
+int vip_kernel_timing_end(void) {
+    g_timing.on = false;
+    return g_timing.n;
+}
+
+int vip_kernel_timing_get(int index, float* ms, char* name, size_t len) {
+    KernelTiming& t = g_timing;
+    if (index < 0 || index >= t.n || t.on || !ms) return VIP_ERR_INVALID_ARGUMENT;
+    VIP_HIP_CHECK(hipEventSynchronize(t.ev[2 * index + 1]));
+    VIP_HIP_CHECK(hipEventElapsedTime(ms, t.ev[2 * index], t.ev[2 * index + 1]));
+    if (name && len) {
+        const std::string s = kernel_name(t.kern[index]);
+        const size_t n = s.size() < len - 1 ? s.size() : len - 1;
+        std::memcpy(name, s.data(), n);
+        name[n] = 0;
+    }
+    return 0;
 }
 
 int vip_abi_version(void) { return VIP_ABI_VERSION; }

@@ -4,6 +4,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <atomic>
 #include <cstddef>
 #include <cstdint>
@@ -92,6 +93,26 @@ inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned 
 // texture-stage kernel notes its host stub before its launch, so a caller can name the
 // exact template instantiation it timed (bench.py matches it against PMC summaries).
 void note_launch(const void* kern);
+
+// Kernel-duration recorder of the calling thread (vip_kernel_timing_*, vip_capi.hip): while
+// it is on, the (start, stop) events for the next launch of `kern`, else two nulls.
+struct LaunchEvents {
+    hipEvent_t start, stop;
+};
+LaunchEvents timing_events(const void* kern);
+
+// Every stencil and texture launch goes through here: with the recorder on, the launch
+// carries an event pair that the runtime stamps with the kernel's own begin and end
+// (hipExtLaunchKernel: no marker packet enters the stream, so the duration is the one
+// rocprofv3 --kernel-trace reports); otherwise a plain launch.
+template <typename K, typename... Args>
+inline void launch(K kern, dim3 grid, dim3 block, uint32_t lds, hipStream_t stream, Args... args) {
+    const LaunchEvents ev = timing_events(reinterpret_cast<const void*>(kern));
+    if (ev.start)
+        hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev.start, ev.stop, 0u, args...);
+    else
+        hipLaunchKernelGGL(kern, grid, block, lds, stream, args...);
+}
 
 // vip_bilateral_set_waves (vip_capi.hip): 0 = per-launch choice, else 16 / 8 / 4.
 int bilateral_forced_waves();

@@ -276,7 +276,7 @@ static int launch_rt_c(const RtArgs& a, int lds, hipStream_t stream) {
     const long long tiles = (long long)a.tiles_x * tiles_y;
     if (tiles == 0) return 0;
     if (tiles > 0x7fffffffLL) return VIP_ERR_INVALID_ARGUMENT;
-    hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(kRtWaves * 64), lds, stream, a);
+    launch(kern, dim3((unsigned)tiles), dim3(kRtWaves * 64), lds, stream, a);
     return (int)hipGetLastError();
 }
 

@@ -66,7 +66,7 @@ __global__ __launch_bounds__(256) void gradient_kernel(const T* __restrict__ src
 template <typename T, int CH, bool FMA>
 static int launch_gradient_t(const T* src, float* dst, int width, int height, hipStream_t stream) {
     dim3 grid((width + 63) / 64, (height + 3) / 4);
-    hipLaunchKernelGGL((gradient_kernel<T, CH, FMA>), grid, dim3(256), 0, stream, src, dst, width, height);
+    launch(gradient_kernel<T, CH, FMA>, grid, dim3(256), 0, stream, src, dst, width, height);
     return (int)hipGetLastError();
 }
 
@@ -151,10 +151,10 @@ int launch_blur_rtv(const uint8_t* img, const float* mag, float* blurred, float*
     const int lds = (kBlurTW + 2 * radius) * (kBlurTH + 2 * radius) * 8;
     dim3 grid((width + kBlurTW - 1) / kBlurTW, (height + kBlurTH - 1) / kBlurTH);
     if (cpp)
-        hipLaunchKernelGGL(blur_rtv_kernel<true>, grid, dim3(256), lds, stream, img, mag, blurred, rtv, width, height,
+        launch(blur_rtv_kernel<true>, grid, dim3(256), lds, stream, img, mag, blurred, rtv, width, height,
                            ksize);
     else
-        hipLaunchKernelGGL(blur_rtv_kernel<false>, grid, dim3(256), lds, stream, img, mag, blurred, rtv, width, height,
+        launch(blur_rtv_kernel<false>, grid, dim3(256), lds, stream, img, mag, blurred, rtv, width, height,
                            ksize);
     return (int)hipGetLastError();
 }
@@ -218,9 +218,9 @@ int launch_guide(const float* blurred, const float* rtv, uint8_t* guide, int wid
     const int lds = (kBlurTW + 2 * radius) * (kBlurTH + 2 * radius) * 4;
     dim3 grid((width + kBlurTW - 1) / kBlurTW, (height + kBlurTH - 1) / kBlurTH);
     if (cpp)
-        hipLaunchKernelGGL(guide_kernel<true>, grid, dim3(256), lds, stream, blurred, rtv, guide, width, height, ksize);
+        launch(guide_kernel<true>, grid, dim3(256), lds, stream, blurred, rtv, guide, width, height, ksize);
     else
-        hipLaunchKernelGGL(guide_kernel<false>, grid, dim3(256), lds, stream, blurred, rtv, guide, width, height, ksize);
+        launch(guide_kernel<false>, grid, dim3(256), lds, stream, blurred, rtv, guide, width, height, ksize);
     return (int)hipGetLastError();
 }
 
@@ -870,7 +870,7 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int 
     note_launch(reinterpret_cast<const void*>(kern));
     if (gy1 <= gy0) return 0;
     dim3 grid((width + G::TW - 1) / G::TW, (gy1 - gy0 + G::TH - 1) / G::TH);
-    hipLaunchKernelGGL(kern, grid, dim3(G::NT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
+    launch(kern, grid, dim3(G::NT), LDS, stream, img, guide, width, lo, hi, gy0, gy1, ksize, aligned);
     return (int)hipGetLastError();
 }
 
@@ -1045,7 +1045,7 @@ int launch_texture_iteration_fused(const StencilArgs& a, int ksize, bool cpp, hi
     args.tiles_x = (a.width + FuJG::TW - 1) / FuJG::TW;
     args.tiles_total = args.tiles_x * ((a.out_rows + kFuTH - 1) / kFuTH);
     if (args.tiles_total == 0) return 0;
-    hipLaunchKernelGGL(kern, dim3(args.tiles_total), dim3(kFuNT), kFuLds, stream, args, ksize);
+    launch(kern, dim3(args.tiles_total), dim3(kFuNT), kFuLds, stream, args, ksize);
     return (int)hipGetLastError();
 }
 

@@ -29,7 +29,7 @@ from ._lib import VIP_NUMERICS_CPP, VIP_NUMERICS_CUDA, VipError, call, lib
 __all__ = [
     "CudaBilateralFilter", "CudaAdaptiveBilateralFilter", "CudaBilateralTextureFilter", "cuda_gradient",
     "DeviceImage", "VipError", "VIP_NUMERICS_CUDA", "VIP_NUMERICS_CPP", "device_synchronize",
-    "set_bilateral_waves", "set_bilateral_wide", "set_bilateral_frames_in_flight", "launched_kernels", "set_stencil_path", "max_ksize",
+    "set_bilateral_waves", "set_bilateral_wide", "set_bilateral_frames_in_flight", "launched_kernels", "kernel_timing", "set_stencil_path", "max_ksize",
 ]
 
 
@@ -113,6 +113,38 @@ def launched_kernels() -> list:
     buf = ctypes.create_string_buffer(n + 1)
     lib().vip_launched_kernels(buf, n + 1)
     return [x for x in buf.value.decode().split("\n") if x]
+
+
+class kernel_timing:
+    """include/vip.h vip_kernel_timing_*: inside ``with kernel_timing(capacity) as kt:`` the
+    next `capacity` kernels this thread launches through the library carry events the
+    runtime stamps with each kernel's own begin and end (hipExtLaunchKernel). Afterwards
+    ``kt.records()`` gives [(kernel name, ms)] in launch order and ``kt.durations()``
+    {kernel name: [ms, ...]}; both wait for the kernels to finish."""
+
+    def __init__(self, capacity: int):
+        self.capacity = int(capacity)
+        self.count = 0
+
+    def __enter__(self):
+        call("vip_kernel_timing_begin", self.capacity)
+        return self
+
+    def __exit__(self, *exc):
+        self.count = int(lib().vip_kernel_timing_end())
+
+    def records(self) -> list:
+        out, ms, name = [], ctypes.c_float(), ctypes.create_string_buffer(512)
+        for i in range(self.count):
+            call("vip_kernel_timing_get", i, ctypes.byref(ms), name, len(name))
+            out.append((name.value.decode(), float(ms.value)))
+        return out
+
+    def durations(self) -> dict:
+        d = {}
+        for n, ms in self.records():
+            d.setdefault(n, []).append(ms)
+        return d
 
 
 def set_bilateral_waves(waves: int = 0) -> None:
