@@ -188,6 +188,22 @@ def native_forms(stream_counts, texture: bool, batches=None) -> list:
     return forms
 
 
+def multi_gpu_wall_estimate_s(config: str, n: int, step_ms: float, steps=None, warmup: int = 20,
+                              settle_s: float = 1.0) -> float:
+    """Worst-case device wall time of one `bench.py --gpus n` line (n > 1, native exchange,
+    no --streams / --batch): the settle, every trial form (NBUF untimed + 48 timed steps, plus
+    ~5 ms of syncs and barriers each), the warm-up, the K timed steps and the K/4 evented
+    steps -- twice for the strong-scaling configs, whose line also measures the weak figure
+    (rank startup, imports and RCCL set-up come on top). step_ms: a rank's ms per step in
+    that config at that n (the loopback rehearsal lines)."""
+    cfg = CONFIGS[config]
+    k = DEFAULT_STEPS[config] if steps is None else steps
+    forms = native_forms(TRIAL_STREAMS, cfg["kind"] == "texture")
+    per = settle_s + len(forms) * ((NBUF + 48) * step_ms * 1e-3 + 5e-3) + (warmup + k + max(4, k // 4)) * step_ms * 1e-3
+    strong_with_weak = cfg["kind"] != "texture" and "frame_height" not in cfg
+    return per * (2 if strong_with_weak else 1)
+
+
 def single_gpu_forms(stream_counts, batches=None) -> list:
     """The N = 1 trial's forms for the plain and adaptive filters, the same (S, B) grid as
     the N > 1 trial so both lines are timed in the same forms: S streams of frames in
@@ -1352,6 +1368,17 @@ def main():
         **({"batch": m["batch_trial"]} if m.get("batch_trial") else {}),
         **({"weak": weak} if weak else {}),
     }
+    bt = m.get("batch_trial")
+    if world == 1 and bt and bt.get("chosen", 1) > 1:
+        # a shared-launch form won the N = 1 trial (C1): the value is a batched throughput;
+        # the reference times one blocking call per frame (sample/benchmark/main.cpp:20-33),
+        # so the default form's own rate (one frame per launch, the trial's time) sits beside it
+        d_ms = bt["trial_ms_per_step"][bt["default"]]
+        out["throughput_form"] = (f"batched throughput: {bt['streams']} streams x {bt['chosen']} frames per shared "
+                                  f"launch ({m['frames_in_flight']} frames in flight)")
+        out["one_frame_per_launch"] = dict(form=bt["default"], ms_per_step=round(d_ms, 4),
+                                           value=round(total_px / (d_ms * 1e-3) / 1e6, 2),
+                                           source="the N = 1 trial's time of the default form")
     if state["multi"]:
         # an N-GPU line must show that RCCL saw N ranks on N distinct devices
         problems = []

@@ -155,6 +155,33 @@ def test_committed_lines_divide_by_a_kernel_duration_that_fits_a_step():
         assert roofline_duration_fits_a_step(line), (f, line["roofline"]["avg_launch_ms"], line["ms_per_step"])
 
 
+# what one N-GPU bench line may take on the device, startup excluded: the driver runs
+# N = 1, 2, 4, 8 back to back on one node, so each line must stay well inside its limit
+MULTI_GPU_LINE_BUDGET_S = 60.0
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c4", "c5"])
+def test_multi_gpu_trial_wall_time_is_bounded(cfg):
+    """The N > 1 trial: every form the trial times, with the step times
+    of the loopback rehearsals at that N (profiles/r0*_<cfg>_loopback<N>_bench.json), or the
+    N = 1 line's step split N ways (C4: a 2160-row slab per rank, the N = 1 step) where no
+    rehearsal exists, fits MULTI_GPU_LINE_BUDGET_S per line. The N = 8 constants (free CUs,
+    frames per RCCL group) are re-tuned only from the driver's own xGMI lines."""
+    import glob
+
+    def line(path):  # the JSON line (rehearsal files carry RCCL's banner before it)
+        return json.loads([x for x in open(path) if x.startswith("{")][-1])
+    n1 = line(os.path.join(ROOT, "profiles", f"r05_final_{cfg}_bench.json"))["ms_per_step"]
+    for n in (2, 4, 8):
+        got = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r0*_{cfg}_loopback{n}_bench.json")))
+        step = line(got[-1])["ms_per_step"] if got else (n1 if cfg == "c4" else n1 / n)
+        step = max(step, n1 if cfg == "c4" else n1 / n)  # never below linear
+        t = bench.multi_gpu_wall_estimate_s(cfg, n, step * 1.5)  # xGMI exchange slower than loopback: 1.5x
+        assert t < MULTI_GPU_LINE_BUDGET_S, (cfg, n, step, t)
+    assert len(bench.native_forms(bench.TRIAL_STREAMS, False)) == 48
+    assert len(bench.native_forms(bench.TRIAL_STREAMS, True)) == 9
+
+
 def test_halo_batches_keep_buffers_on_one_stream():
     """bench.py N > 1 native path: frame i in batch i // B on stream (i // B) % S. For
     every batch size it may choose, each buffer (i % NBUF) always meets the same stream,

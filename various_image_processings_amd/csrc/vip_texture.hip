@@ -283,9 +283,12 @@ constexpr int kGfRun = 4;  // guide: vertically adjacent outputs per thread
 
 constexpr int cmax(int a, int b) { return a > b ? a : b; }
 
-template <int R, int TW_, int TH_, int NT_>
+// MRSEP_: the magnitudes get their own region beside XR (written as they are computed, no
+// barrier between pass 1 and their store), when two workgroups still fit a CU.
+template <int R, int TW_, int TH_, int NT_, bool MRSEP_ = false>
 struct GfGeomT {
     static constexpr int TW = TW_, TH = TH_, NT = NT_;
+    static constexpr bool MRSEP = MRSEP_;
     static_assert(TW % 4 == 0 && TH % 4 == 0, "guide tile: 4-pixel groups, 4-row runs");
     static constexpr int K = 2 * R + 1;
     static constexpr int BW = TW + 2 * R;               // BR/RR: T (+) R
@@ -301,20 +304,31 @@ struct GfGeomT {
     static constexpr int XR_WORDS = XW * XH;
     static constexpr int HPL = HWP * HH;                // one H plane
     static constexpr int BPL = BW * BHP;                // one BR/RR plane
-    // XR, then MR in its place (gradients wait in registers until XR is consumed);
-    // H after it (RB, MX words + G as u16); BR/RR and the guide tile GT reuse it all
-    static constexpr int A_WORDS = cmax(XR_WORDS + 2 * HPL + HPL / 2, 4 * BPL + TW * TH);
+    // XR, then MR in its place (gradients wait in registers until XR is consumed) or, with
+    // MRSEP, beside it; H after them (RB, MX words + G as u16); BR/RR and the guide tile GT
+    // reuse it all
+    static constexpr int MR_AT = MRSEP ? XR_WORDS : 0;
+    static constexpr int H_AT = XR_WORDS + (MRSEP ? MW * MH : 0);
+    static constexpr int A_WORDS = cmax(H_AT + 2 * HPL + HPL / 2, 4 * BPL + TW * TH);
     static constexpr int WORDS = A_WORDS;
     // the exp table (64 doubles) after every region, read by the guide phase
     static constexpr int ETAB = round_up(WORDS, 4);
     static constexpr int WORDS_ALL = ETAB + 128;
-    static_assert(MW * MH <= XR_WORDS, "MR reuses the XR region");
+    static_assert(MRSEP || MW * MH <= XR_WORDS, "MR reuses the XR region");
     static constexpr int NR1 = HH * (HWP / kGfH1);      // pass-1 runs
     static constexpr int NR2 = BW * (BHP / kGfV2);      // pass-2 runs
     static constexpr int IT2 = (NR2 + NT - 1) / NT;
 };
+// Measurement knob VIP_GF_MR_SEP: MR beside XR at R = 2 (92 x 36: 80,224 bytes, still two
+// workgroups per CU), one barrier and the MR store phase fewer -- bit-exact and slower:
+// 67.8-68.3 against 65.4-65.9 us per 4K launch, interleaved (profiles/r06_guide_barrier_cuts_ab.txt)
+#ifdef VIP_GF_MR_SEP
+constexpr bool kGfMrSep2 = true;
+#else
+constexpr bool kGfMrSep2 = false;
+#endif
 template <int R>
-using GfGeom = GfGeomT<R, gf_tile(R).tw, gf_tile(R).th, gf_tile(R).nt>;
+using GfGeom = GfGeomT<R, gf_tile(R).tw, gf_tile(R).th, gf_tile(R).nt, R == 2 && kGfMrSep2>;
 
 typedef short gf_s16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short gf_u16x2 __attribute__((ext_vector_type(2)));
@@ -386,11 +400,11 @@ __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restr
                              // uses sigma_alpha = 1/(5 ksize) even when ksize is even
     constexpr bool PACKRB = K * K * 255 < 65536;  // R|B<<16 vertical sums stay in 16 bits
     uint32_t* XR = lds;
-    uint32_t* H = lds + G::XR_WORDS;                    // RB plane, MX plane (HPL words each)
+    uint32_t* H = lds + G::H_AT;                        // RB plane, MX plane (HPL words each)
     uint16_t* HG = reinterpret_cast<uint16_t*>(H + 2 * G::HPL);  // G sums (<= K * 255) as u16
     float* BR = reinterpret_cast<float*>(lds);          // 3 planes of BPL, aliases XR/H
     float* RR = BR + 3 * G::BPL;
-    float* MR = reinterpret_cast<float*>(lds);  // written once XR is consumed
+    float* MR = reinterpret_cast<float*>(lds + G::MR_AT);  // (aliased: written once XR is consumed)
     double* const etab = reinterpret_cast<double*>(lds + G::ETAB);  // kExp2Tab64
     // OPAQUE_TID (the fused iteration kernel, which calls this three times): without it
     // the compiler keeps chunk 0's thread-index arithmetic live across the later chunks
@@ -464,7 +478,7 @@ VIP_GF_STAMP(8);
     //     integer (< 2^24), equal to the reference's float sums: v_dot2 on the
     //     {c0, c2} 16-bit difference pairs, a mad for c1.
     constexpr int NM = G::MW * G::MH, KM = (NM + G::NT - 1) / G::NT;
-    float mrv[KM];  // this thread's gradients, stored to MR (over XR) after pass 1
+    float mrv[G::MRSEP ? 1 : KM];  // aliased MR: this thread's gradients, stored over XR after pass 1
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
         VIP_GF_PROGRESS(k * 4 / KM);
@@ -481,10 +495,14 @@ VIP_GF_STAMP(8);
         const int ss = __builtin_amdgcn_sdot2(h02, h02, __builtin_amdgcn_sdot2(v02, v02, h1 * h1 + v1 * v1, false),
                                               false);
 #ifdef VIP_GF_LLVM_SQRT  // the compiler's correctly rounded expansion (same result, 17 VALU)
-        mrv[k] = __builtin_sqrtf((float)ss);
+        const float mag = __builtin_sqrtf((float)ss);
 #else
-        mrv[k] = sqrt_int_exact((float)ss);  // == sqrtf, exhaustively checked (microbench/div_check)
+        const float mag = sqrt_int_exact((float)ss);  // == sqrtf, exhaustively checked (microbench/div_check)
 #endif
+        if constexpr (G::MRSEP)
+            MR[i] = mag;
+        else
+            mrv[k] = mag;
     }
     VIP_GF_STAMP(9);
     // 2b. pass 1: H = horizontal K-window aggregates, kGfH1 adjacent columns per thread.
@@ -519,15 +537,17 @@ VIP_GF_STAMP(8);
     }
     VIP_GF_STAMP(2);
     __syncthreads();  // XR is consumed (gradients and pass 1): MR takes its place
-    VIP_GF_PROGRESS(0);
+    if constexpr (!G::MRSEP) {
+        VIP_GF_PROGRESS(0);
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-        const int i = tid + k * G::NT;
-        if (NM % G::NT != 0 && i >= NM) continue;
-        MR[i] = mrv[k];
+        for (int k = 0; k < KM; ++k) {
+            const int i = tid + k * G::NT;
+            if (NM % G::NT != 0 && i >= NM) continue;
+            MR[i] = mrv[k];
+        }
+        VIP_GF_STAMP(3);
+        __syncthreads();
     }
-    VIP_GF_STAMP(3);
-    __syncthreads();
 
     // 3. pass 2: blur + mRTV at the BR positions, kGfV2 vertically adjacent positions per
     //    thread (vertical windows of H, magnitude sums in row-major order). Blur
@@ -825,6 +845,30 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
     const int tid = threadIdx.x;
     const int W1 = width - 1;
     VIP_GF_STAMP(0);
+#ifdef VIP_GF_DIRECT_STORE
+    // measurement knob: guide words straight to HBM -- a quad of lanes holds 4 horizontally
+    // adjacent pixels (the guide runs are column-major in the lanes, TW % 4 == 0), lanes 0-2
+    // of the quad store one dword each of the 12 bytes; byte stores at a ragged edge or an
+    // unaligned buffer. No guide tile in LDS and no barrier after the guide phase; bit-exact
+    // and 1 us slower per launch on top of VIP_GF_MR_SEP (profiles/r06_guide_barrier_cuts_ab.txt).
+    static_assert(G::TW % 4 == 0, "whole quads per guide row");
+    guide_tile<G, R, CPP>(lds, img, width, lo, hi, gy1, ksize, aligned, x0, y0, [&](int ty, int tx, uint32_t gw) {
+        const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)gw, 0xF9, 0xF, 0xF, false);  // quad_perm 1,2,3,3
+        const int q = tx & 3, xq = x0 + tx - q;
+        uint8_t* const orow = guide + ((long long)(y0 + ty) * width + xq) * 3;
+        if ((aligned & 2) && xq + 3 <= W1) {
+            if (q < 3) reinterpret_cast<uint32_t*>(orow)[q] = (gw >> (8 * q)) | (nx << (24 - 8 * q));
+        } else {
+            uint8_t* const o = orow + 3 * q;
+            o[0] = (uint8_t)gw;
+            o[1] = (uint8_t)(gw >> 8);
+            o[2] = (uint8_t)(gw >> 16);
+        }
+    });
+    (void)tid;
+    VIP_GF_STAMP(6);
+    VIP_GF_STAMP(7);
+#else  // the guide tile through LDS, one barrier, then dword rows
     uint32_t* GT = lds + 4 * G::BPL;  // guide tile as RGBX words, after BR/RR
     guide_tile<G, R, CPP>(lds, img, width, lo, hi, gy1, ksize, aligned, x0, y0,
                           [&](int ty, int tx, uint32_t gw) { GT[ty * G::TW + tx] = gw; });
@@ -856,6 +900,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
         }
     }
     VIP_GF_STAMP(7);
+#endif
 }
 
 template <int R, bool CPP>
@@ -874,9 +919,358 @@ static int launch_gf(const uint8_t* img, uint8_t* guide, int width, int lo, int 
     return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Streaming guide stage, R = 2 (ksize 4 and 5: C4) -- built, bit-exact, and SLOWER: 90.1
+// against 65.0 us per 4K launch (profiles/r06_guide_stage_ab.txt), so it is a build knob
+// (VIP_GF_STREAM), not the default. The rings cost 52 KiB per 512-thread workgroup, so only
+// two workgroups share a CU at its 121 VGPRs (three at 80 VGPRs spill: 126.8 us); the guide
+// and pass-2 phases then run on 2 of a SIMD's 4 waves, where the tiled stage runs each phase
+// on all 8 -- the phases' LDS and f64 latency chains are no longer hidden. Same arithmetic
+// as guide_tile, same bytes; a different schedule. One workgroup walks down a strip of GsTW output columns over
+// a segment of rows, kGsV rows per step, and every phase of the stage is in flight in every
+// step, each on its own row group (a software pipeline with one barrier per step):
+//   A  image rows [Y0 + 5 + sV, +V): global loads issued at the top of step s, written to the
+//      XR ring at its end (the loads fly under the step's compute)
+//   B  rows [Y0 + 4 + (s-1)V, +V): gradient magnitudes (MR ring) and the horizontal K-window
+//      aggregates of pass 1 (H ring), from XR rows stored by step s - 1
+//   C  rows [Y0 + 2 + (s-2)V, +V): pass 2, box blur + mRTV (BR/RR rings), from H/MR rows of
+//      step s - 1 (vertical windows of H, magnitude sums in the reference's row-major order)
+//   D  rows [Y0 + (s-3)V, +V): the guide (first strict argmin, alpha blend) from BR/RR rows
+//      of step s - 1, straight to HBM (a quad of lanes assembles 4 RGB pixels into 3 dwords)
+// Each stage lags the one it reads by exactly the rows it needs (V + 1 rows for B, V + R for
+// C and D), so one step of lag suffices and the rings hold 10 (XR) and 12 rows (the rest).
+// The vertical apron is paid once per segment instead of once per tile: 1.03 blur positions
+// and 1.06 gradients per output against the tiled stage's 1.16 and 1.33. The waves take
+// roles: 0-1 the guide, 2-3 pass 2, 4-6 gradients and loads, 7 pass 1 -- two heavy and one
+// or two light waves per SIMD, so no SIMD idles while a phase of another runs alone.
+// Rings hold only rows in [lo, hi) (slot = row mod ring size); every reader clamps its row
+// index, as the reference clamps its coordinates. Columns stay pre-clamped (XR holds the
+// pixel at the clamped column, so MR, H and BR/RR hold the values at clamped centres).
+// ---------------------------------------------------------------------------
+namespace gs {
+constexpr int R = 2, K = 2 * R + 1, V = 4;
+constexpr int TW = 124, NT = 512;        // output columns per strip; 8 waves
+constexpr int BW = TW + 2 * R;           // 128 blur / H columns: image x0 - R + c
+constexpr int MW = TW + 4 * R;           // 132 magnitude columns: image x0 - 2R + c
+constexpr int XL = 8;                    // XR column 0 = image x0 - XL (4-pixel aligned)
+constexpr int XG = 35, XW = 4 * XG;      // 140 XR words per row: image x0 - 8 .. x0 + 131
+constexpr int XRING = 10, RING = 12;     // ring rows
+constexpr int O_XR = 0;
+constexpr int O_MR = O_XR + XRING * XW;
+constexpr int O_HRB = O_MR + RING * MW;  // R | B << 16 window sums
+constexpr int O_HMX = O_HRB + RING * BW; // max s | (1023 - min s) << 16, s = r + g + b
+constexpr int O_HG = O_HMX + RING * BW;  // G window sums, u16
+constexpr int O_BR = O_HG + RING * BW / 2;
+constexpr int O_RR = O_BR + 3 * RING * BW;
+constexpr int O_ET = round_up(O_RR + RING * BW, 2);
+constexpr int WORDS = O_ET + 128;        // + the exp table (64 doubles)
+constexpr int LDS = 4 * WORDS;           // 52,384 bytes: three workgroups per CU
+constexpr int NGRAD = V * MW;            // 528 gradients per step (waves 4-6, <= 3 each)
+constexpr int NLOAD = V * XG;            // 140 four-pixel loads per step (waves 4-6)
+static_assert(TW % 4 == 0 && TW <= 128 && BW == 128, "guide on waves 0-1, pass 2 on waves 2-3");
+static_assert(V * (BW / 8) == 64, "pass 1 on wave 7: one run of 8 columns per lane");
+static_assert(NGRAD <= 3 * 192 && NLOAD <= 192, "gradients and loads on waves 4-6");
+static_assert(XW - XL >= TW + 2 * R + 2 && XW % 4 == 0, "XR covers the gradient and pass-1 reads");
+static_assert(3 * LDS <= kLdsBudget, "three workgroups per CU");
+constexpr int kMinSegRows = 16;          // rows per segment at least (the apron is ~10 rows)
+}  // namespace gs
+
+#ifdef VIP_GS_WAVES_PER_EU  // measurement knob: cap the VGPRs so more workgroups share a CU
+#define VIP_GS_OCC __attribute__((amdgpu_waves_per_eu(VIP_GS_WAVES_PER_EU, VIP_GS_WAVES_PER_EU)))
+#else
+#define VIP_GS_OCC
+#endif
+template <bool CPP>
+__global__ __launch_bounds__(gs::NT) VIP_GS_OCC void texture_guide_stream_kernel(const uint8_t* __restrict__ img,
+                                                                      uint8_t* __restrict__ guide, int width, int lo,
+                                                                      int hi, int gy0, int gy1, int seg_rows,
+                                                                      int ksize, int aligned) {
+    using namespace gs;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* const XR = lds + O_XR;
+    float* const MR = reinterpret_cast<float*>(lds + O_MR);
+    uint32_t* const HRB = lds + O_HRB;
+    uint32_t* const HMX = lds + O_HMX;
+    uint16_t* const HG = reinterpret_cast<uint16_t*>(lds + O_HG);
+    float* const BR = reinterpret_cast<float*>(lds + O_BR);  // 3 planes of RING x BW
+    float* const RR = reinterpret_cast<float*>(lds + O_RR);
+    double* const etab = reinterpret_cast<double*>(lds + O_ET);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int x0 = blockIdx.x * TW, xr0 = x0 - XL;
+    const int Y0 = gy0 + blockIdx.y * seg_rows;
+    const int Y1 = Y0 + seg_rows < gy1 ? Y0 + seg_rows : gy1;
+    if (Y0 >= Y1) return;  // whole workgroup
+    const int W1 = width - 1, H1 = hi - 1;
+    // rows each stage produces (the guide rows' reach, clamped to the valid rows)
+    const int as = Y0 - 2 * R - 1 > lo ? Y0 - 2 * R - 1 : lo, ae = Y1 + 2 * R + 1 < hi ? Y1 + 2 * R + 1 : hi;
+    const int bs = Y0 - 2 * R > lo ? Y0 - 2 * R : lo, be = Y1 + 2 * R < hi ? Y1 + 2 * R : hi;
+    const int cs = Y0 - R > lo ? Y0 - R : lo, ce = Y1 + R < hi ? Y1 + R : hi;
+    if (tid < 64) etab[tid] = kExp2Tab64[tid];  // first read by D at step 3, after barriers
+    const float kk = (float)(ksize * ksize);
+    const float rkk = 1.f / kk;
+    constexpr float kThird = 0x1.555556p-2f;  // RN(1/3)
+    const float sigma_alpha = 1.f / (float)(5 * ksize);
+    const int ngroups = (Y1 - Y0 + V - 1) / V;
+
+    for (int s = -3; s < ngroups + 3; ++s) {
+        // ---- A: issue this step's image loads (waves 4-6) ----
+        uint32_t raw0 = 0, raw1 = 0, raw2 = 0;
+        int xr_at = -1;  // XR word the loaded group goes to
+        if (wave >= 4 && wave < 7) {
+            const int i = tid - 256;
+            if (i < NLOAD) {
+                const int rr = i / XG, gx = i - rr * XG;
+                const int r = Y0 + 2 * R + 1 + s * V + rr;
+                if (r >= as && r < ae) {
+                    const uint8_t* row = img + (long long)r * width * 3;
+                    const int x = xr0 + 4 * gx;
+                    if ((aligned & 1) && x >= 0 && x + 3 <= W1) {
+                        const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
+                        raw0 = w[0];
+                        raw1 = w[1];
+                        raw2 = w[2];
+                    } else {
+                        const uint32_t q0 = load_rgb(row, clampi(x, 0, W1)), q1 = load_rgb(row, clampi(x + 1, 0, W1));
+                        const uint32_t q2 = load_rgb(row, clampi(x + 2, 0, W1)), q3 = load_rgb(row, clampi(x + 3, 0, W1));
+                        raw0 = q0 | (q1 << 24);
+                        raw1 = (q1 >> 8) | (q2 << 16);
+                        raw2 = (q2 >> 16) | (q3 << 8);
+                    }
+                    xr_at = (r % XRING) * XW + 4 * gx;
+                }
+            }
+        }
+
+        if (wave < 2) {
+            // ---- D: guide rows [g0, g0 + V) ----
+            const int g0 = Y0 + (s - 3) * V;
+            if (s >= 3) {
+                const int tx = lane + 64 * wave;
+                const int txr = tx < TW ? tx : TW - 1;  // lanes past the strip read in-strip values
+                // window rows g0 - R .. g0 + V - 1 + R (clamped): each row's minimum and the
+                // first column holding it (rtv >= +0 and finite: bit patterns order like values)
+                uint32_t rv[V + 2 * R];
+                int ri[V + 2 * R];
+#pragma unroll
+                for (int t = 0; t < V + 2 * R; ++t) {
+                    const int row = clampi(g0 - R + t, lo, H1);
+                    const int base = (row % RING) * BW + txr;
+                    uint32_t m[K];
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) m[kx] = __float_as_uint(RR[base + kx]);
+                    uint32_t v = m[0];
+#pragma unroll
+                    for (int kx = 1; kx < K; ++kx) v = v < m[kx] ? v : m[kx];
+                    rv[t] = v;
+                    int c = K - 1;
+#pragma unroll
+                    for (int kx = K - 2; kx >= 0; --kx) c = m[kx] == v ? kx : c;
+                    ri[t] = base + c;
+                }
+                const int x = x0 + tx;
+                const int q = lane & 3;
+                // a quad of lanes = 4 pixels = 3 dwords (lanes 0-2 store one each); whole
+                // quads are in or out of the strip (TW % 4 == 0)
+                const bool dword_quad = (aligned & 2) && tx - q + 3 < TW && x - q + 3 <= W1;
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int g = g0 + j;
+                    if (g >= Y1) break;
+                    uint32_t mb = rv[j];
+#pragma unroll
+                    for (int ky = 1; ky < K; ++ky) mb = mb < rv[j + ky] ? mb : rv[j + ky];
+                    int mi = ri[j + K - 1];
+#pragma unroll
+                    for (int ky = K - 2; ky >= 0; --ky) mi = rv[j + ky] == mb ? ri[j + ky] : mi;
+                    const float rmin = __uint_as_float(mb);
+                    const int ci = (g % RING) * BW + txr + R;
+                    const float arg = sigma_alpha * (RR[ci] - rmin);
+                    const float e = exp_tab_f32(arg, etab);  // == (float)exp((double)arg)
+                    const float alpha = 2.f * recip_exact(1.f + e) - 1.f;
+                    const float beta = 1.f - alpha;
+                    uint32_t gw = 0;
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float bm = BR[c * RING * BW + mi], bc = BR[c * RING * BW + ci];
+                        const float v = CPP ? (alpha * bm + beta * bc) + 0.5f : __builtin_fmaf(alpha, bm, beta * bc) + 0.5f;
+                        gw = pack_u8_clamped(v, c, gw);  // == clampi((int)v, 0, 255) << 8c
+                    }
+                    // the next lane's pixel (quad_perm [1, 2, 3, 3])
+                    const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)gw, 0xF9, 0xF, 0xF, false);
+                    uint8_t* const orow = guide + ((long long)g * width + (x - q)) * 3;
+                    if (dword_quad) {
+                        if (q < 3)
+                            reinterpret_cast<uint32_t*>(orow)[q] = (gw >> (8 * q)) | (nx << (24 - 8 * q));
+                    } else if (tx < TW && x <= W1) {
+                        uint8_t* const o = orow + 3 * q;
+                        o[0] = (uint8_t)gw;
+                        o[1] = (uint8_t)(gw >> 8);
+                        o[2] = (uint8_t)(gw >> 16);
+                    }
+                }
+            }
+        } else if (wave < 4) {
+            // ---- C: pass 2 at blur rows [p0, p0 + V), column bc ----
+            const int p0 = Y0 + R + (s - 2) * V;
+            if (p0 + V > cs && p0 < ce) {
+                const int bc = tid - 128;
+                // the blur centre's clamped column: its H column and its MR window's first column
+                const int hcol = clampi(x0 - R + bc, 0, W1) - (x0 - R);
+                constexpr int NV = V + K - 1;
+                uint32_t hrb[NV], hg[NV], hmx[NV], rowmax[NV];
+                int hro[NV];
+#pragma unroll
+                for (int t = 0; t < NV; ++t) {
+                    hro[t] = clampi(p0 - R + t, lo, H1) % RING;
+                    hrb[t] = HRB[hro[t] * BW + hcol];
+                    hg[t] = HG[hro[t] * BW + hcol];
+                    hmx[t] = HMX[hro[t] * BW + hcol];
+                }
+                uint32_t s0[V], s1[V], smx[V], mmaxb[V];
+                float msum[V];
+                win_sum<V, K>(hrb, s0);
+                win_sum<V, K>(hg, s1);
+                win_op<V, K>(hmx, smx, pk_max_u16);
+#pragma unroll
+                for (int t = 0; t < NV; ++t) {
+                    const float* mrow = MR + hro[t] * MW + hcol;
+                    float m[K];
+#pragma unroll
+                    for (int kx = 0; kx < K; ++kx) m[kx] = mrow[kx];
+                    uint32_t mx = __float_as_uint(m[0]);
+#pragma unroll
+                    for (int kx = 1; kx < K; ++kx) {  // == the reference's max (no NaN, >= +0)
+                        const uint32_t b = __float_as_uint(m[kx]);
+                        mx = mx > b ? mx : b;
+                    }
+                    rowmax[t] = mx;
+#pragma unroll
+                    for (int j = 0; j < V; ++j) {  // window row t - j of position j, row-major
+                        if (t - j < 0 || t - j >= K) continue;
+                        msum[j] = t == j ? m[0] : msum[j] + m[0];
+#pragma unroll
+                        for (int kx = 1; kx < K; ++kx) msum[j] = msum[j] + m[kx];
+                    }
+                }
+                win_op<V, K>(rowmax, mmaxb, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+#pragma unroll
+                for (int j = 0; j < V; ++j) {
+                    const int p = p0 + j;
+                    if (p < cs || p >= ce) continue;
+                    const int o = (p % RING) * BW + bc;
+                    BR[o] = div_exact(s0[j] & 0xffffu, kk, rkk);
+                    BR[RING * BW + o] = div_exact(s1[j], kk, rkk);
+                    BR[2 * RING * BW + o] = div_exact(s0[j] >> 16, kk, rkk);
+                    const float imax = div_exact(smx[j] & 0xffffu, 3.f, kThird);
+                    const float imin = div_exact(1023u - (smx[j] >> 16), 3.f, kThird);
+                    const float num = (imax - imin) * __uint_as_float(mmaxb[j]);
+                    RR[o] = CPP ? num / (msum[j] + 1e-9f) : (float)((double)num / ((double)msum[j] + 1e-9));
+                }
+            }
+        } else {
+            const int b0 = Y0 + 2 * R + (s - 1) * V;
+            if (b0 + V > bs && b0 < be) {
+                if (wave < 7) {
+                    // ---- B: gradient magnitudes at rows [b0, b0 + V), MR columns ----
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const int i = tid - 256 + k * 192;
+                        if (i >= NGRAD) break;
+                        const int rr = i / MW, mc = i - rr * MW;
+                        const int r = b0 + rr;
+                        if (r < bs || r >= be) continue;
+                        const int cx = clampi(x0 - 2 * R + mc, 0, W1) - xr0;
+                        const uint32_t* rc = XR + (r % XRING) * XW + cx;
+                        const uint32_t U = XR[((r - 1 > lo ? r - 1 : lo) % XRING) * XW + cx];
+                        const uint32_t D = XR[((r + 1 < H1 ? r + 1 : H1) % XRING) * XW + cx];
+                        const uint32_t L = rc[-1], Rt = rc[1];
+                        const gf_s16x2 h02 = __builtin_bit_cast(gf_s16x2, Rt & 0x00ff00ffu) -
+                                             __builtin_bit_cast(gf_s16x2, L & 0x00ff00ffu);
+                        const gf_s16x2 v02 = __builtin_bit_cast(gf_s16x2, D & 0x00ff00ffu) -
+                                             __builtin_bit_cast(gf_s16x2, U & 0x00ff00ffu);
+                        const int h1 = (int)__builtin_amdgcn_ubfe(Rt, 8, 8) - (int)__builtin_amdgcn_ubfe(L, 8, 8);
+                        const int v1 = (int)__builtin_amdgcn_ubfe(D, 8, 8) - (int)__builtin_amdgcn_ubfe(U, 8, 8);
+                        const int ss = __builtin_amdgcn_sdot2(
+                            h02, h02, __builtin_amdgcn_sdot2(v02, v02, h1 * h1 + v1 * v1, false), false);
+                        MR[(r % RING) * MW + mc] = sqrt_int_exact((float)ss);  // == sqrtf
+                    }
+                } else {
+                    // ---- B: pass 1, H at row b0 + lane / 16, columns 8 (lane % 16) .. +8 ----
+                    const int r = b0 + (lane >> 4), hc0 = (lane & 15) * 8;
+                    if (r >= bs && r < be) {
+                        const uint32_t* xrow = XR + (r % XRING) * XW + hc0 + XL - 2 * R;
+                        constexpr int NX = 8 + K - 1;
+                        uint32_t rb[NX], gg[NX], mx[NX];
+#pragma unroll
+                        for (int t = 0; t < NX; ++t) {
+                            const uint32_t p = xrow[t];
+                            const uint32_t sb = __builtin_amdgcn_sad_u8(p, 0u, 0u);  // r + g + b
+                            rb[t] = p & 0x00ff00ffu;
+                            gg[t] = __builtin_amdgcn_ubfe(p, 8, 8);
+                            mx[t] = ((sb ^ 1023u) << 16) | sb;  // max of lo = max s, of hi = 1023 - min s
+                        }
+                        uint32_t orb[8], og[8], omx[8];
+                        win_sum<8, K>(rb, orb);
+                        win_sum<8, K>(gg, og);
+                        win_op<8, K>(mx, omx, pk_max_u16);
+                        const int o = (r % RING) * BW + hc0;
+                        *reinterpret_cast<uint4*>(HG + o) = make_uint4(og[0] | (og[1] << 16), og[2] | (og[3] << 16),
+                                                                       og[4] | (og[5] << 16), og[6] | (og[7] << 16));
+#pragma unroll
+                        for (int j = 0; j < 8; j += 4) {
+                            *reinterpret_cast<uint4*>(HRB + o + j) = make_uint4(orb[j], orb[j + 1], orb[j + 2], orb[j + 3]);
+                            *reinterpret_cast<uint4*>(HMX + o + j) = make_uint4(omx[j], omx[j + 1], omx[j + 2], omx[j + 3]);
+                        }
+                    }
+                }
+            }
+        }
+        // ---- A: the loaded image group into the XR ring ----
+        if (xr_at >= 0) *reinterpret_cast<uint4*>(XR + xr_at) = unpack_rgb4(raw0, raw1, raw2);
+        __syncthreads();
+    }
+}
+
+// Segments per strip: as many as fill the workgroup slots of the device in one round (the
+// runtime's occupancy for this kernel: LDS and VGPRs), each at least kMinSegRows rows (the
+// pipeline's apron is about ten rows).
+template <bool CPP>
+static int launch_gs(const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1, int ksize,
+                     int aligned, hipStream_t stream) {
+    auto kern = texture_guide_stream_kernel<CPP>;
+    static std::atomic<unsigned long long> attr_devs{0};
+    if (const int rc = ensure_dynamic_lds(reinterpret_cast<const void*>(kern), gs::LDS, attr_devs)) return rc;
+    note_launch(reinterpret_cast<const void*>(kern));
+    if (gy1 <= gy0) return 0;
+    static std::atomic<int> per_cu{0};  // workgroups per CU (the same on every MI355X)
+    int wg = per_cu.load(std::memory_order_relaxed);
+    if (wg == 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&wg, reinterpret_cast<const void*>(kern), gs::NT, gs::LDS) !=
+                hipSuccess ||
+            wg < 1)
+            wg = 1;
+        per_cu.store(wg, std::memory_order_relaxed);
+    }
+    const int rows = gy1 - gy0;
+    const int strips = (width + gs::TW - 1) / gs::TW;
+    const int slots = wg * device_cus();
+    int nseg = slots / strips;
+    const int max_seg = (rows + gs::kMinSegRows - 1) / gs::kMinSegRows;
+    nseg = nseg < 1 ? 1 : (nseg > max_seg ? max_seg : nseg);
+    const int seg_rows = (rows + nseg - 1) / nseg;
+    nseg = (rows + seg_rows - 1) / seg_rows;
+    launch(kern, dim3(strips, nseg), dim3(gs::NT), gs::LDS, stream, img, guide, width, lo, hi, gy0, gy1, seg_rows,
+           ksize, aligned);
+    return (int)hipGetLastError();
+}
+
 template <bool CPP>
 static int launch_gf_r(int ksize, const uint8_t* img, uint8_t* guide, int width, int lo, int hi, int gy0, int gy1,
                        int aligned, hipStream_t s) {
+#ifdef VIP_GF_STREAM  // measurement knob: the streaming stage at R = 2 (bit-exact, 1.39x slower)
+    if (ksize / 2 == 2) return launch_gs<CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
+#endif
 #ifdef VIP_GF_ONLY_R2  // quick variant builds (scripts/build_texture_variant.sh): k = 4, 5 only
     if (ksize / 2 == 2) return launch_gf<2, CPP>(img, guide, width, lo, hi, gy0, gy1, ksize, aligned, s);
     return VIP_ERR_UNSUPPORTED_KSIZE;
