@@ -30,7 +30,8 @@ def lib() -> ctypes.CDLL:
         L.ref_guide.argtypes = [vp, vp, vp, i, i, i]
         L.ref_gradient_u8.argtypes = [vp, vp, i, i, i]
         L.ref_gradient_f32.argtypes = [vp, vp, i, i, i]
-        for fn in ("ref_adaptive", "ref_blur_rtv", "ref_guide", "ref_gradient_u8", "ref_gradient_f32"):
+        L.ref_cpp_luts.argtypes = [i, f, f, i, vp, vp]
+        for fn in ("ref_adaptive", "ref_blur_rtv", "ref_guide", "ref_gradient_u8", "ref_gradient_f32", "ref_cpp_luts"):
             getattr(L, fn).restype = None
         _lib = L
     return _lib
@@ -77,3 +78,12 @@ def gradient(src):
     fn = lib().ref_gradient_u8 if src.dtype == np.uint8 else lib().ref_gradient_f32
     fn(src.ctypes.data, dst.ctypes.data, w, h, ch)
     return dst
+
+
+def cpp_luts(ksize, sigma_space, sigma_color, color_len=768):
+    """internal::pre_compute_kernels (include/cpp/bilateral_filter.hpp:10-39): the include/cpp
+    filters' space LUT (ksize x ksize) and colour LUT (768, or 1536 for the adaptive filter)."""
+    space = np.empty((ksize, ksize), np.float32)
+    color = np.empty(color_len, np.float32)
+    lib().ref_cpp_luts(ksize, sigma_space, sigma_color, color_len, space.ctypes.data, color.ctypes.data)
+    return space, color

@@ -5,6 +5,7 @@ exists): outputs of the reference tests' OWN CPU oracles, compiled where they li
   RefAdaptiveBilateralFilterImpl   test/adaptive_bilateral_filter.cu:7-119
   RefBilateralTextureFilterImpl    test/bilateral_texture_filter.cu:8-113 (blur/rtv, guide)
   ref_gradient<T>                  test/gradient.cu:9-34
+  internal::pre_compute_kernels    include/cpp/bilateral_filter.hpp:10-39 (the include/cpp LUTs)
 
 on the reference tests' own inputs (test/random_array.hpp, seed 42, 50x50: the inputs every
 gtest case of those files builds) at ksize 9 (their default) and 15, plus one 640x360 frame
@@ -26,6 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 SMALL_K = (9, 15)
+# include/cpp LUT sets (ksize, sigma_space, sigma_color, colour LUT length): the bilateral
+# defaults, BASELINE C2/C5, the largest ksize, a narrow sigma, and the adaptive filter's 1536
+LUT_CASES = ((9, 10.0, 30.0, 768), (15, 10.0, 30.0, 768), (31, 20.0, 60.0, 768), (65, 10.0, 30.0, 768),
+             (9, 4.0, 1.73205080757, 768), (15, 10.0, 30.0, 1536), (63, 10.0, 30.0, 1536))
 CHAIN_K = (5, 9)
 OUT = os.path.join(HERE, "ref_oracles.npz")
 
@@ -70,6 +75,16 @@ def compute(ref, x, lenna):
     return out
 
 
+def compute_luts(luts):
+    """luts(ksize, sigma_space, sigma_color, color_len) -> (space, colour), per LUT_CASES."""
+    out = {}
+    for k, ss, sc, n in LUT_CASES:
+        sp, co = luts(k, ss, sc, n)
+        out[f"cpp_lut_space_k{k}_s{ss:g}_c{sc:g}_n{n}"] = np.asarray(sp, np.float32).reshape(k, k)
+        out[f"cpp_lut_color_k{k}_s{ss:g}_c{sc:g}_n{n}"] = np.asarray(co, np.float32)
+    return out
+
+
 def main():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
     from oracle import oracle as o
@@ -78,6 +93,7 @@ def main():
         raise SystemExit("oracle/_ref/libref_test_oracles.so missing: /root/reference not mounted?")
     lenna = np.load(os.path.join(HERE, "lenna_bgr.npz"))["bgr"]
     out = compute(ref, inputs(o), lenna)
+    out.update(compute_luts(ref.cpp_luts))
     np.savez_compressed(OUT, **out)
     print("wrote", len(out), "entries to", os.path.relpath(OUT, ROOT))
 

@@ -75,11 +75,20 @@ def test_fixture_covers_every_reference_oracle(fixture):
     assert fixture["adaptive_k9"].shape == (50, 50, 3) and fixture["guide_k15"].dtype == np.uint8
 
 
+def test_cpp_profile_luts_equal_the_reference_lut_builder(oracle, fixture):
+    """The CPP profile's space and colour LUTs (vipo_space_lut / vipo_color_lut) equal
+    include/cpp's internal::pre_compute_kernels, compiled from the reference, bit for bit
+    (bilateral 768, adaptive 1536 entries, ksize up to 65)."""
+    got = mrg.compute_luts(lambda k, ss, sc, n: (oracle.space_lut(k, ss, oracle.CPP), oracle.color_lut(n, sc, oracle.CPP)))
+    assert len(got) == 2 * len(mrg.LUT_CASES)
+    assert [k for k in got if not np.array_equal(got[k], fixture[k])] == []
+
+
 def test_ref_profile_equals_the_reference_oracles(oracle, fixture, computed):
     """Every entry -- adaptive, gradient u8/f32 x 1/3 ch, blur/rtv, guide, the 640x360 chain,
     adaptive on lenna -- bit for bit."""
     out = computed[oracle.REF]
-    bad = [k for k in fixture if not np.array_equal(fixture[k], out[k])]
+    bad = [k for k in fixture if not k.startswith("cpp_lut") and not np.array_equal(fixture[k], out[k])]
     assert not bad, bad
 
 
@@ -123,5 +132,6 @@ def test_fixture_is_what_the_reference_oracles_compute_now(fixture, inputs, lenn
     """Re-derive the fixture from the compiled reference oracles: the committed file is current."""
     from oracle import ref_test_oracles as ref
     live = mrg.compute(ref, inputs, lenna)
+    live.update(mrg.compute_luts(ref.cpp_luts))
     assert sorted(live) == sorted(fixture)
     assert [k for k in live if not np.array_equal(live[k], fixture[k])] == []
