@@ -189,7 +189,7 @@ def native_forms(stream_counts, texture: bool, batches=None) -> list:
 
 
 def multi_gpu_wall_estimate_s(config: str, n: int, step_ms: float, steps=None, warmup: int = 20,
-                              settle_s: float = 1.0) -> float:
+                              settle_s: float = 6.0) -> float:
     """Worst-case device wall time of one `bench.py --gpus n` line (n > 1, native exchange,
     no --streams / --batch): the settle, every trial form (NBUF untimed + 48 timed steps, plus
     ~5 ms of syncs and barriers each), the warm-up, the K timed steps and the K/4 evented
@@ -266,7 +266,10 @@ def parse():
     # MI355X clocks ramp over ~1 s of sustained load (measured, C2 r=7 4K: 0.219 ms per
     # frame after 3 warm-up steps, 0.179 ms after 200): keep launching untimed steps for
     # this long before the W warm-up steps so the timed steps see the steady clock
-    p.add_argument("--settle-s", type=float, default=1.0)
+    # this long before the W warm-up steps so the timed steps see the steady clock. 6 s, not
+    # the 1 s the clocks need: a process-external sampler reading GPU activity every ~5 s
+    # (the driver's rocm-smi) then sees the device busy in at least one sample
+    p.add_argument("--settle-s", type=float, default=6.0)
     p.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     # rehearsal only: gloo + every rank on cuda:0 runs the N>1 code path on a 1-GPU box

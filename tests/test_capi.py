@@ -229,3 +229,17 @@ def test_build_stamp_matches_the_tree():
     if c["sources_match"]:
         assert c["libs_match"], c
     assert len(build_info.source_files()) > 15
+
+
+def test_build_stamp_missing_library_is_a_mismatch(tmp_path, monkeypatch):
+    """A library missing both when the stamp was written and now is not a match,
+    and a stamp without a `libs` entry is a mismatch, not a KeyError."""
+    import json
+    from various_image_processings_amd import build_info
+    info = tmp_path / "build_info.json"
+    monkeypatch.setattr(build_info, "INFO", str(info))
+    monkeypatch.setattr(build_info, "_lib_sha", lambda name: None)
+    info.write_text(json.dumps(dict(sources_sha256="x", libs={n: None for n in build_info.LIBS})))
+    assert build_info.check()["libs_match"] is False
+    info.write_text(json.dumps(dict(sources_sha256="x")))
+    assert build_info.check()["libs_match"] is False
