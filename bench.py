@@ -198,7 +198,7 @@ def multi_gpu_wall_estimate_s(config: str, n: int, step_ms: float, steps=None, w
     that config at that n (the loopback rehearsal lines)."""
     cfg = CONFIGS[config]
     k = DEFAULT_STEPS[config] if steps is None else steps
-    forms = native_forms(TRIAL_STREAMS, cfg["kind"] == "texture")
+    forms = native_forms(TRIAL_STREAMS, cfg["kind"] == "texture", cfg.get("native_batches"))
     per = settle_s + len(forms) * ((NBUF + 48) * step_ms * 1e-3 + 5e-3) + (warmup + k + max(4, k // 4)) * step_ms * 1e-3
     strong_with_weak = cfg["kind"] != "texture" and "frame_height" not in cfg
     return per * (2 if strong_with_weak else 1)
@@ -238,7 +238,11 @@ CONFIGS = {
     # c5 at N = 1: one 805 MB frame per launch (4 rounds of 256 workgroups over 8,192 tiles), so
     # sharing a launch between frames cannot remove a tail worth timing; the N = 1 trial keeps
     # 2 streams and one frame per launch
+    # N > 1: one frame per RCCL group (native_batches): a rank's slab is 8192 / 4096 / 2048 rows at
+    # N = 2 / 4 / 8, 3-13 ms a step, so shared launches have no tail to remove and the 48-form
+    # grid alone would take ~40 s at N = 2 (tests/test_bench_contract.py wall-time bound)
     "c5": dict(kind="bilateral", width=16384, frame_height=16384, ksize=31, single_gpu_forms=[(2, 1)],
+               native_batches=[1],
                workload="bilateral r=15 16384x16384 RGB8 row-tiled"),
     # not a BASELINE config: the largest ksize the reference runs (its shared memory
     # fits CUDA's 48 KB default up to 65), on the runtime-radius kernel
@@ -915,6 +919,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     # indices run nothing; buffer i % NBUF keeps its stream)
     i_settle = align(i_settle)
     batches = None if args.batch is None else [args.batch]
+    native_batches = batches if batches is not None else cfg.get("native_batches")
     if native and not has_peers:
         # one rank (--rehearse-native): no halo moves, so split / batch forms would only
         # time noise between identical launches; keep the defaults and say so
@@ -931,7 +936,7 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
         # flight hide one stream's exchange latency behind the others' launches.
         trial = {}
         n_trial = 48  # a multiple of every B
-        forms = native_forms(s_forms, cfg["kind"] == "texture", batches)
+        forms = native_forms(s_forms, cfg["kind"] == "texture", native_batches)
         if not forms:
             raise SystemExit(f"bench.py: --batch {args.batch} fits none of the stream counts {s_forms}")
         for n_s, split, b, shared in forms:
