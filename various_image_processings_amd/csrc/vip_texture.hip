@@ -384,6 +384,63 @@ __device__ unsigned long long vip_gf_stamps[4096 * 16 * 16];
 #define VIP_GF_PROGRESS(band)
 #endif
 
+// Phase 1 of a guide tile. issue() starts the global loads of the XR region of the tile with origin (x0, y0) into
+// registers (4-pixel groups, dword loads when interior and aligned, clamped bytes otherwise;
+// every load of the thread issued before any is unpacked: one HBM latency per tile, not one
+// per group), commit() unpacks them into XR as RGBX words.
+template <class G, int R>
+struct XrLoad {
+    static constexpr int NG = G::XH * (G::XW / 4);
+    static constexpr int KG = (NG + G::NT - 1) / G::NT;
+    uint32_t raw[KG][3];
+
+    __device__ __forceinline__ void issue(const uint8_t* __restrict__ img, int width, int lo, int hi, int aligned,
+                                          int x0, int y0, int tid) {
+        const int xr0 = x0 - G::XL, yr0 = y0 - 2 * R - 1;
+        const int W1 = width - 1;
+#pragma unroll
+        for (int k = 0; k < KG; ++k) {
+            const int g = tid + k * G::NT;
+            if (NG % G::NT != 0 && g >= NG) continue;
+            const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
+            const uint8_t* row = img + (long long)clampi(yr0 + ry, lo, hi - 1) * width * 3;
+            const int x = xr0 + 4 * gx;
+#ifdef VIP_GF_ABL_LOAD  // timing ablation only (wrong output): no HBM reads
+            if (true) {
+                raw[k][0] = g * 0x01010101u;
+                raw[k][1] = (g + x) * 0x01010101u;
+                raw[k][2] = (g ^ 7) * 0x01010101u;
+            } else
+#endif
+#ifdef VIP_GF_ISA_HOT  // ISA-count builds only (scripts/isa_classes.py): the interior path alone
+            if (true) {
+#else
+            if ((aligned & 1) && x >= 0 && x + 3 <= W1) {
+#endif
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
+                raw[k][0] = w[0];
+                raw[k][1] = w[1];
+                raw[k][2] = w[2];
+            } else {
+                const uint32_t q0 = load_rgb(row, clampi(x, 0, W1)), q1 = load_rgb(row, clampi(x + 1, 0, W1));
+                const uint32_t q2 = load_rgb(row, clampi(x + 2, 0, W1)), q3 = load_rgb(row, clampi(x + 3, 0, W1));
+                raw[k][0] = q0 | (q1 << 24);
+                raw[k][1] = (q1 >> 8) | (q2 << 16);
+                raw[k][2] = (q2 >> 16) | (q3 << 8);
+            }
+        }
+    }
+    __device__ __forceinline__ void commit(uint32_t* XR, int tid) const {
+#pragma unroll
+        for (int k = 0; k < KG; ++k) {
+            const int g = tid + k * G::NT;
+            if (NG % G::NT != 0 && g >= NG) continue;
+            const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
+            *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = unpack_rgb4(raw[k][0], raw[k][1], raw[k][2]);
+        }
+    }
+};
+
 // Row bands: rows [lo, hi) of the (dense, width*3 pitch) buffers are the valid
 // frame rows -- every stage clamps into them, as the reference clamps into
 // [0, height) -- and guide rows [gy0, gy1) are produced (a row slab of a sharded
@@ -393,6 +450,9 @@ __device__ unsigned long long vip_gf_stamps[4096 * 16 * 16];
 // the G::WORDS words of LDS at `lds`; rows >= gy1 and columns past the image are not
 // produced. Each guide word (RGBX) goes to sink(ty, tx, word), tile-relative. Ends
 // after the guide phase WITHOUT a barrier (the caller's sink target decides).
+// (A persistent guide kernel that issues its next tile's XrLoad right before the guide phase
+// needs 72 more VGPRs than the 64 of two workgroups per CU and spills them: measured in round
+// 6 at the compiler's resource report, not built.)
 template <class G, int R, bool CPP, bool OPAQUE_TID = false, class Sink>
 __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restrict__ img, int width, int lo, int hi,
                                            int gy1, int ksize, int aligned, int x0, int y0, Sink&& sink) {
@@ -420,58 +480,18 @@ __device__ __forceinline__ void guide_tile(uint32_t* lds, const uint8_t* __restr
     const int mr0x = x0 - 2 * R, mr0y = y0 - 2 * R;
     const int W1 = width - 1, H0 = lo, H1 = hi - 1;
 
-    // 1. XR: 4-pixel groups, dword loads when interior and aligned, clamped bytes
-    //    otherwise; every load of the thread is issued before the first is unpacked
-    //    (one HBM latency per tile, not one per group)
+    // 1. XR: 4-pixel groups (XrLoad)
     {
-        constexpr int NG = G::XH * (G::XW / 4);
-        constexpr int KG = (NG + G::NT - 1) / G::NT;
-        uint32_t raw[KG][3];
-#pragma unroll
-        for (int k = 0; k < KG; ++k) {
-            const int g = tid + k * G::NT;
-            if (NG % G::NT != 0 && g >= NG) continue;
-            const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
-            const uint8_t* row = img + (long long)clampi(yr0 + ry, H0, H1) * width * 3;
-            const int x = xr0 + 4 * gx;
-#ifdef VIP_GF_ABL_LOAD  // timing ablation only (wrong output): no HBM reads
-            if (true) {
-                raw[k][0] = g * 0x01010101u;
-                raw[k][1] = (g + x) * 0x01010101u;
-                raw[k][2] = (g ^ 7) * 0x01010101u;
-            } else
-#endif
-#ifdef VIP_GF_ISA_HOT  // ISA-count builds only (scripts/isa_classes.py): the interior path alone
-            if (true) {
-#else
-            if ((aligned & 1) && x >= 0 && x + 3 <= W1) {
-#endif
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(row + 3 * x);
-                raw[k][0] = w[0];
-                raw[k][1] = w[1];
-                raw[k][2] = w[2];
-            } else {
-                const uint32_t q0 = load_rgb(row, clampi(x, 0, W1)), q1 = load_rgb(row, clampi(x + 1, 0, W1));
-                const uint32_t q2 = load_rgb(row, clampi(x + 2, 0, W1)), q3 = load_rgb(row, clampi(x + 3, 0, W1));
-                raw[k][0] = q0 | (q1 << 24);
-                raw[k][1] = (q1 >> 8) | (q2 << 16);
-                raw[k][2] = (q2 >> 16) | (q3 << 8);
-            }
-        }
-VIP_GF_STAMP(8);
+        XrLoad<G, R> xl;
+        xl.issue(img, width, lo, hi, aligned, x0, y0, tid);
+        VIP_GF_STAMP(8);
 #ifndef VIP_GF_EXP_OCML
         if (tid < 64) etab[tid] = kExp2Tab64[tid];  // read in phase 4, after several barriers
 #endif
-#pragma unroll
-        for (int k = 0; k < KG; ++k) {
-            const int g = tid + k * G::NT;
-            if (NG % G::NT != 0 && g >= NG) continue;
-            const int ry = g / (G::XW / 4), gx = g - ry * (G::XW / 4);
-            *reinterpret_cast<uint4*>(XR + ry * G::XW + 4 * gx) = unpack_rgb4(raw[k][0], raw[k][1], raw[k][2]);
-        }
+        xl.commit(XR, tid);
+        VIP_GF_STAMP(1);
+        __syncthreads();
     }
-    VIP_GF_STAMP(1);
-    __syncthreads();
 
     // 2a. MR[q] = gradient at c = clamp(q); XR is pre-clamped, so c's neighbours are
     //     read directly (XR[c +- e] == X(clamp(c +- e))). sum_c h^2 + v^2 is an exact
@@ -834,6 +854,36 @@ VIP_GF_STAMP(8);
     }
 }
 
+// 5. guide tile -> HBM: 4 RGBX words -> 3 dwords per thread (byte stores at a ragged right
+//    edge or an unaligned buffer)
+template <class G>
+__device__ __forceinline__ void store_guide_tile(const uint32_t* GT, uint8_t* __restrict__ guide, int width, int x0,
+                                                 int y0, int gy1, int aligned, int tid) {
+    const int W1 = width - 1;
+    for (int q = tid; q < G::TH * (G::TW / 4); q += G::NT) {
+        const int gr = q / (G::TW / 4), x = x0 + 4 * (q - gr * (G::TW / 4));
+        const int y = y0 + gr;
+        if (y >= gy1 || x > W1) continue;
+        const uint4 w = *reinterpret_cast<const uint4*>(GT + gr * G::TW + (x - x0));
+        uint8_t* row = guide + ((long long)y * width + x) * 3;
+        if ((aligned & 2) && x + 3 <= W1) {
+            uint32_t* d = reinterpret_cast<uint32_t*>(row);
+            d[0] = w.x | (w.y << 24);
+            d[1] = (w.y >> 8) | (w.z << 16);
+            d[2] = (w.z >> 16) | (w.w << 8);
+        } else {
+            const uint32_t ws_[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (x + i > W1) break;
+                row[3 * i] = (uint8_t)ws_[i];
+                row[3 * i + 1] = (uint8_t)(ws_[i] >> 8);
+                row[3 * i + 2] = (uint8_t)(ws_[i] >> 16);
+            }
+        }
+    }
+}
+
 template <int R, bool CPP>
 __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
                                                                    uint8_t* __restrict__ guide, int width, int lo,
@@ -875,30 +925,7 @@ __global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(cons
     VIP_GF_STAMP(6);
     __syncthreads();
 
-    // 5. guide tile -> HBM: 4 RGBX words -> 3 dwords per thread (byte stores at a
-    //    ragged right edge or an unaligned buffer)
-    for (int q = tid; q < G::TH * (G::TW / 4); q += G::NT) {
-        const int gr = q / (G::TW / 4), x = x0 + 4 * (q - gr * (G::TW / 4));
-        const int y = y0 + gr;
-        if (y >= gy1 || x > W1) continue;
-        const uint4 w = *reinterpret_cast<const uint4*>(GT + gr * G::TW + (x - x0));
-        uint8_t* row = guide + ((long long)y * width + x) * 3;
-        if ((aligned & 2) && x + 3 <= W1) {
-            uint32_t* d = reinterpret_cast<uint32_t*>(row);
-            d[0] = w.x | (w.y << 24);
-            d[1] = (w.y >> 8) | (w.z << 16);
-            d[2] = (w.z >> 16) | (w.w << 8);
-        } else {
-            const uint32_t ws_[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                if (x + i > W1) break;
-                row[3 * i] = (uint8_t)ws_[i];
-                row[3 * i + 1] = (uint8_t)(ws_[i] >> 8);
-                row[3 * i + 2] = (uint8_t)(ws_[i] >> 16);
-            }
-        }
-    }
+    store_guide_tile<G>(GT, guide, width, x0, y0, gy1, aligned, tid);
     VIP_GF_STAMP(7);
 #endif
 }
