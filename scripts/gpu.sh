@@ -30,7 +30,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 O=gpurun_out
 
 fail() { echo "step '$1' failed rc=$2"; [ -n "${3:-}" ] && tail -25 "$3"; exit "$2"; }
@@ -61,8 +61,11 @@ for step in "$@"; do
       rc=$?; cut -c1-600 $out; [ $rc -eq 0 ] || fail "$step" $rc $O/${TAG}_${cfg}_bench.err ;;
     stats)
       cfg=${A[0]}; steps=20; [ $cfg = c5 ] && steps=5; d=$O/prof_${TAG}_$cfg
+      # one stream and a 1 s settle: the summary's average is then a launch duration (with two
+      # streams the launches overlap and the settle's queued frames dominate the count)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
-        python bench.py --config $cfg --steps $steps --warmup 3 --no-cpu-baseline --batch 1 "${A[@]:1}" > $d.log 2>&1
+        python bench.py --config $cfg --steps $steps --warmup 3 --no-cpu-baseline --streams 1 --batch 1 \
+        --settle-s 1 "${A[@]:1}" > $d.log 2>&1
       rc=$?; [ $rc -eq 0 ] || fail "$step" $rc $d.log
       cp $d/run_kernel_stats.csv $O/${TAG}_${cfg}_kernel_stats.csv
       python scripts/kernel_busy.py $d/run_kernel_trace.csv $O/${TAG}_${cfg}_busy.json > /dev/null || fail "$step" $?
