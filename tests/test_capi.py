@@ -243,3 +243,17 @@ def test_build_stamp_missing_library_is_a_mismatch(tmp_path, monkeypatch):
     assert build_info.check()["libs_match"] is False
     info.write_text(json.dumps(dict(sources_sha256="x")))
     assert build_info.check()["libs_match"] is False
+
+
+def test_kernel_timing_validates_before_device_work():
+    """vip_kernel_timing_*: capacity outside 1..65536 is refused before any device call; a read
+    with nothing recorded (or while recording) is refused; end reports the launches recorded."""
+    import ctypes
+    from various_image_processings_amd import _lib
+    lib = _lib.lib()
+    assert lib.vip_kernel_timing_begin(0) == 10001
+    assert lib.vip_kernel_timing_begin(1 << 17) == 10001
+    assert lib.vip_kernel_timing_end() == 0
+    ms = ctypes.c_float()
+    assert lib.vip_kernel_timing_get(0, ctypes.byref(ms), None, 0) == 10001
+    assert lib.vip_kernel_timing_get(-1, ctypes.byref(ms), None, 0) == 10001
