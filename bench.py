@@ -897,9 +897,12 @@ def measure(args, cfg, frame_h, torch, dev, rank, world, streams, state, s_forms
     # agreed by rank 0.
     t_settle, i_settle = time.perf_counter(), 0
     if not multi:
+        # one stream: back-to-back launches warm the clocks as well as overlapped ones, and a
+        # kernel trace of the run (rocprofv3, the driver's own profile) then shows launch
+        # durations rather than spans of launches sharing the chip
         while time.perf_counter() - t_settle < args.settle_s:
             for _ in range(8):
-                run(i_settle, streams[i_settle % S], i_settle % S)
+                run(i_settle, streams[0], 0)
                 i_settle += 1
             torch.cuda.synchronize(dev)
     else:
