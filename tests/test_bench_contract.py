@@ -372,14 +372,16 @@ def test_c1_shared_launch_sample():
 @pytest.mark.parametrize("cfg", sorted(ISO_KERNELS))
 def test_isolated_launch_samples_are_large_enough(cfg):
     """the launch duration behind each headline roofline rests on a
-    committed single-stream rocprofv3 sample (profiles/r05_<cfg>_isolated.csv, via
+    committed single-stream rocprofv3 sample (profiles/r0N_<cfg>_isolated.csv, via
     scripts/isolated_sample.py) of at least 200 launches of the exact instantiation, and the
-    committed line's live event-timed launch agrees with it to 3 %."""
+    same round's committed line's live launch duration agrees with it to 3 %."""
     for kern in ISO_KERNELS[cfg]:
         s = bench.isolated_sample(cfg, kern)
         assert s is not None and s["launches"] >= 200, (cfg, kern, s)
         assert s["min_us"] <= s["median_us"] <= s["max_us"]
-    line = json.loads(open(os.path.join(ROOT, "profiles", f"r05_{cfg}_bench.json")).read().strip().splitlines()[-1])
+    # the committed line of the same round as the newest sample (profiles/rNN_<cfg>_bench.json)
+    rnd = os.path.basename(bench.isolated_sample(cfg, ISO_KERNELS[cfg][0])["source"]).split("_")[0]
+    line = json.loads(open(os.path.join(ROOT, "profiles", f"{rnd}_{cfg}_bench.json")).read().strip().splitlines()[-1])
     r = line["roofline"]
     if cfg == "c4":  # the JBF launch (the guide stage's instantiation carries its argument list)
         launch_ms = [k["avg_launch_ms"] for k in (r["dominant"], r["other"]) if "joint" in k["kernel"]][0]
