@@ -270,12 +270,59 @@ namespace vip {
 // 661.7-667.2 (96 x 36 668-671, 124 x 24 673, 108 x 32 678-680, 80 x 40 697, 80 x 44 692,
 // 60 x 60 693). VIP_GF_TW / _TH / _NT override R <= 2.
 struct GfTile { int tw, th, nt; };
+// Tiles per radius for R > 2 (texture ksize 6..24; the reference's default ksize 9 is R = 4).
+// Round 6, kernel-stamped 4K launches interleaved on one box against the 64 x 16 / 256-thread
+// tile (profiles/r06_guide_tiles_big_r_ab{,2}.txt): R = 3 92 x 32 / 1024 110.7 -> 91.1 us (fewer
+// blur positions per output: 1.33 against 1.64); R = 4 the same tile with its VGPRs capped at 64
+// (two workgroups per CU, 10 spilled) 134.4 -> 110.5; R = 5 92 x 32 216.6 -> 192.3 (uncapped:
+// capped spills 37 and runs 211.5); R = 6 keeps 64 x 16 (60 x 36: 300.5, capped 261.6 against
+// 263.8); R = 7 60 x 36 capped (49 spilled) 446.7 -> 394.5. Knobs: VIP_GF_T<R> = GfTile{tw, th,
+// nt}, VIP_GF_WPE<R> = minimum waves per SIMD (8 caps the VGPRs at 64).
+#ifndef VIP_GF_T3
+#define VIP_GF_T3 GfTile{92, 32, 1024}
+#endif
+#ifndef VIP_GF_T4
+#define VIP_GF_T4 GfTile{92, 32, 1024}
+#endif
+#ifndef VIP_GF_T5
+#define VIP_GF_T5 GfTile{92, 32, 1024}
+#endif
+#ifndef VIP_GF_T6
+#define VIP_GF_T6 GfTile{64, 16, 256}
+#endif
+#ifndef VIP_GF_T7
+#define VIP_GF_T7 GfTile{60, 36, 1024}
+#endif
+#ifndef VIP_GF_WPE4
+#define VIP_GF_WPE4 8
+#endif
+#ifndef VIP_GF_WPE5
+#define VIP_GF_WPE5 1
+#endif
+#ifndef VIP_GF_WPE6
+#define VIP_GF_WPE6 1
+#endif
+#ifndef VIP_GF_WPE7
+#define VIP_GF_WPE7 8
+#endif
 constexpr GfTile gf_tile(int R) {
 #if defined(VIP_GF_TW) && defined(VIP_GF_TH) && defined(VIP_GF_NT)
-    return R <= 2 ? GfTile{VIP_GF_TW, VIP_GF_TH, VIP_GF_NT} : GfTile{64, 16, 256};
+    if (R <= 2) return GfTile{VIP_GF_TW, VIP_GF_TH, VIP_GF_NT};
 #else
-    return R <= 2 ? GfTile{92, 36, 1024} : GfTile{64, 16, 256};
+    if (R <= 2) return GfTile{92, 36, 1024};
 #endif
+    switch (R) {
+        case 3: return VIP_GF_T3;
+        case 4: return VIP_GF_T4;
+        case 5: return VIP_GF_T5;
+        case 6: return VIP_GF_T6;
+        case 7: return VIP_GF_T7;
+        default: return GfTile{64, 16, 256};
+    }
+}
+// minimum waves per SIMD the guide-stage kernel of radius R is compiled for (1: no cap)
+constexpr int gf_min_waves(int R) {
+    return R == 4 ? VIP_GF_WPE4 : R == 5 ? VIP_GF_WPE5 : R == 6 ? VIP_GF_WPE6 : R == 7 ? VIP_GF_WPE7 : 1;
 }
 constexpr int kGfH1 = 8;   // pass 1: horizontally adjacent window aggregates per thread
 constexpr int kGfV2 = 4;   // pass 2: vertically adjacent blur positions per thread
@@ -885,7 +932,8 @@ __device__ __forceinline__ void store_guide_tile(const uint32_t* GT, uint8_t* __
 }
 
 template <int R, bool CPP>
-__global__ __launch_bounds__(GfGeom<R>::NT) void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
+__global__ __launch_bounds__(GfGeom<R>::NT) __attribute__((amdgpu_waves_per_eu(gf_min_waves(R))))
+void texture_guide_fused_kernel(const uint8_t* __restrict__ img,
                                                                    uint8_t* __restrict__ guide, int width, int lo,
                                                                    int hi, int gy0, int gy1, int ksize,
                                                                    int aligned) {
