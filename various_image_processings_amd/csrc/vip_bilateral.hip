@@ -249,8 +249,19 @@ constexpr int lut_copies() {
 #ifndef VIP_BIL_BIG_MAXW
 #define VIP_BIL_BIG_MAXW 16
 #endif
+// Joint filter with 8 outputs per thread beyond radius 7 (VIP_JBF_P8_MAX_R > 7): wave cap
+// (12 waves allow 168 VGPRs: no spills at R = 8..10). Measured round 6 on the texture JBF
+// (profiles/r06_jbf_p8_big_r_ab.txt, 4K, interleaved): R = 8 239.7-240.0 us with 4 outputs
+// on 16 waves against 266.4-266.6 (8 on 12 waves) and 285.9-286.6 (8 on 8); R = 10 379-380
+// against 420 and 449. The default stays 4 outputs beyond radius 7.
+#ifndef VIP_JBF_P8_BIG_MAXW
+#define VIP_JBF_P8_BIG_MAXW 12
+#endif
 template <int R, int PLANES>
-constexpr int max_waves() { return PLANES == 2 ? VIP_JBF_MAXW : (R > 8 ? VIP_BIL_BIG_MAXW : 16); }
+constexpr int max_waves() {
+    return PLANES == 2 ? (R > 7 && R <= VIP_JBF_P8_MAX_R ? VIP_JBF_P8_BIG_MAXW : VIP_JBF_MAXW)
+                       : (R > 8 ? VIP_BIL_BIG_MAXW : 16);
+}
 
 #ifndef VIP_JBF_WIDE  // joint kernel on wide tiles with the 32-copy LUT (measurement knob)
 #define VIP_JBF_WIDE 0
