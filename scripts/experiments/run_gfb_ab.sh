@@ -6,6 +6,6 @@ set -e
 for pass in 1 2; do
   for v in "$@"; do
     echo "== $v"
-    timeout -k 10 300 python scripts/experiments/texture_ksize_bench.py --lib variants/$v.so 7 9 11 13 15
+    timeout -k 10 300 python scripts/experiments/texture_ksize_bench.py --lib variants/$v.so ${KS:-7 9 11 13 15}
   done
 done

@@ -88,10 +88,11 @@ __device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* const lut = lds;
     constexpr int NTAB = FOLD ? disc_r2_count(R) : 1;
-    static_assert(!FOLD || (SAT && NE == 32 && COPIES == 32), "folded tables: saturating address, 32 copies");
+    static_assert(!FOLD || (SAT && NE == 32 && COPIES == sat_fold_copies<R>()), "folded tables: saturating address");
     // SAT: tables from byte SL::T, planes at SL::PL (folded: one table per r^2, d <= DZ;
     // unfolded: the colour LUT, d <= 511, times the spatial weight per tap)
-    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE, FOLD ? disc_r2_count(R) : 1, FOLD ? kSatFoldDz : 511>;
+    using SL = SatLut<R, 4 * (JOINT ? 2 : 1) * PLANE, FOLD ? disc_r2_count(R) : 1, FOLD ? kSatFoldDz : 511,
+                      FOLD ? COPIES : 32>;
     uint32_t* const gplane = SAT ? lds + SL::PL / 4 : lds + NTAB * NE * COPIES;
     uint32_t* const splane = JOINT ? gplane + PLANE : gplane;
 
@@ -174,7 +175,7 @@ __device__ __forceinline__ void bilateral_body(const StencilArgs& a) {
                             uint32_t off = (uint32_t)(SL::T - SL::B0);
                             if constexpr (FOLD) {
                                 constexpr FoldRank<R> rank;
-                                off += 128u * rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)];
+                                off += 4u * COPIES * rank.t[aky * (R + 1) + (kx < 0 ? -kx : kx)];
                             }
                             return sat_addr(d, SL::S, sbias) + off;
                         }
@@ -340,7 +341,7 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream);
 template <int R, int WAVES, int PLANES, int P, bool FOLD>
 constexpr int sat_lds_bytes() {
     return SatLut<R, 4 * PLANES * (WAVES * Geom<R, P>::RPW + 2 * R) * Geom<R, P>::S, FOLD ? disc_r2_count(R) : 1,
-                  FOLD ? kSatFoldDz : 511>::BYTES;
+                  FOLD ? kSatFoldDz : 511, FOLD ? sat_fold_copies<R>() : 32>::BYTES;
 }
 template <int R, int PLANES, int MAXW, int P, bool FOLD>
 constexpr int pick_waves_sat() {
@@ -354,7 +355,7 @@ template <int R, bool JOINT, bool FMA, int NE, bool FOLD = false, bool SAT = fal
 static int launch_bilateral_ne(const StencilArgs& a, hipStream_t stream) {
     constexpr int PLANES = JOINT ? 2 : 1;
     constexpr int P = outputs_per_thread<R, PLANES>();
-    constexpr int COPIES = NE < 768 ? 32 : lut_copies<R, PLANES>();
+    constexpr int COPIES = FOLD ? sat_fold_copies<R>() : NE < 768 ? 32 : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int WAVES = SAT ? pick_waves_sat<R, PLANES, max_waves<R, PLANES>(), P, FOLD>()
                               : pick_waves<R, PLANES, max_waves<R, PLANES>(), LUTW, P>();
@@ -388,9 +389,10 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     constexpr int P = WIDE ? 4 : outputs_per_thread<R, PLANES>();
     constexpr int TPR = WIDE ? 64 : 16;  // threads per tile row
     using G = Geom<R, P, TPR>;
-    constexpr int COPIES = NE < 768 || (WIDE && pick_waves<R, PLANES, WAVES, 768 * 32, P, TPR>() == WAVES)
-                               ? 32
-                               : lut_copies<R, PLANES>();
+    constexpr int COPIES = FOLD ? sat_fold_copies<R>()
+                                : NE < 768 || (WIDE && pick_waves<R, PLANES, WAVES, 768 * 32, P, TPR>() == WAVES)
+                                      ? 32
+                                      : lut_copies<R, PLANES>();
     constexpr int LUTW = (FOLD ? disc_r2_count(R) : 1) * NE * COPIES;
     constexpr int TH = WAVES * G::RPW;
     constexpr int LDS = SAT ? sat_lds_bytes<R, WAVES, PLANES, P, FOLD>() : lds_bytes<R, WAVES, PLANES, LUTW, P, TPR>();
@@ -440,7 +442,8 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
         }
     }
     if constexpr (JOINT && R <= kSatMaxR)  // saturating-address folded tables (SatLut)
-        if (a.fold && a.lut_nonzero <= SatLut<R, 0>::DZ) return launch_bilateral_ne<R, JOINT, FMA, 32, true, true>(a, stream);
+        if (a.fold && a.lut_nonzero <= SatLut<R, 0, disc_r2_count(R), kSatFoldDz, sat_fold_copies<R>()>::DZ)
+            return launch_bilateral_ne<R, JOINT, FMA, 32, true, true>(a, stream);
     if constexpr (JOINT && VIP_JBF_SHORT_LUT)
         if (a.lut_nonzero <= 31) return launch_bilateral_ne<R, JOINT, FMA, 32>(a, stream);
     return launch_bilateral_ne<R, JOINT, FMA, 768>(a, stream);

@@ -25,7 +25,11 @@ constexpr int kWsStride = kMaxRadius + 1; // spatial weights stored as ws[|ky|][
 constexpr int kP = 8;                     // outputs per thread
 constexpr int kTW = 16 * kP;              // tile width in pixels
 constexpr int kLdsBudget = 160 * 1024;
-#ifndef VIP_JBF_SAT_MAX_R  // joint kernel: folded tables behind a saturating address (SatLut) up to this radius
+// joint kernel: folded tables behind a saturating address (SatLut) up to this radius. 7 and 8
+// work with 16-copy tables (sat_fold_copies), bit-exact, but measured slower than the
+// 768 x 16 LUT those radii keep: texture JBF R = 7 186.6 -> 207.8 us, R = 8 242.0 -> 274.7
+// (profiles/r06_jbf_fold16_ab.txt)
+#ifndef VIP_JBF_SAT_MAX_R
 #define VIP_JBF_SAT_MAX_R 6
 #endif
 constexpr int kSatMaxR = VIP_JBF_SAT_MAX_R;
@@ -57,17 +61,32 @@ static_assert(kSatFoldDz < kFoldEntries, "folded tables hold d < kFoldEntries");
 // NTAB_ = 1, DZMAX = 511: the unfolded colour LUT of the plain filter (zero from d <= 511,
 // e.g. sigma_color 30: zero from 432) as 512 entries x 32 copies -- 64 KiB instead of 96,
 // the v_lshl_or of the address replaced by the (fast-class) v_mad_legacy_u16.
-template <int R, int PB, int NTAB_ = disc_r2_count(R), int DZMAX = kSatFoldDz>
+// COPIES_ (round 6): 16 instead of 32 copies per table halve S, so the 16-bit address reaches
+// twice the distances -- the folded tables of radius 7 and 8 (24 and 30 of them) then still
+// hold d <= 31 >= 25, the texture JBF's zero point, where 32 copies stop at 21 and 17. Lanes l
+// and l + 16 of a half-wave then share a copy (<= 2-way bank conflicts, as the 768 x 16 LUT
+// those radii used before); the last copy is 4 * (COPIES - 1) bytes into an entry.
+template <int R, int PB, int NTAB_ = disc_r2_count(R), int DZMAX = kSatFoldDz, int COPIES_ = 32>
 struct SatLut {
     static constexpr int NTAB = NTAB_;
-    static constexpr int S = NTAB * 128;
-    static constexpr int DZ = (65535 - 124) / S < DZMAX ? (65535 - 124) / S : DZMAX;  // tables hold d <= DZMAX
-    static constexpr int B0 = 65535 - DZ * S - 124;
+    static constexpr int COPIES = COPIES_;
+    static constexpr int S = NTAB * 4 * COPIES;
+    static constexpr int LAST = 4 * (COPIES - 1);
+    static constexpr int DZ = (65535 - LAST) / S < DZMAX ? (65535 - LAST) / S : DZMAX;  // tables hold d <= DZMAX
+    static constexpr int B0 = 65535 - DZ * S - LAST;
     static constexpr int T = round_up(B0, 16);
     static constexpr int PL = PB <= B0 ? 0 : round_up(T + (DZ + 1) * S, 16);  // plane offset
     static constexpr int BYTES = PB <= B0 ? T + (DZ + 1) * S : PL + PB;
-    static_assert(DZ >= 0 && T - B0 + (NTAB - 1) * 128 <= 65535, "ds_read immediate range");
+    static_assert(COPIES == 16 || COPIES == 32, "copies");
+    static_assert(DZ >= 0 && T - B0 + (NTAB - 1) * 4 * COPIES <= 65535, "ds_read immediate range");
 };
+// Copies of the joint kernel's folded tables at radius R: 32 (conflict-free) up to R = 6, 16
+// beyond (the address range, above)
+template <int R>
+constexpr int sat_fold_copies() { return R <= 6 ? 32 : 16; }
+static_assert(SatLut<6, 0>::DZ >= 25 && SatLut<8, 0, disc_r2_count(8), kSatFoldDz, 16>::DZ >= 25 &&
+                  SatLut<7, 0, disc_r2_count(7), kSatFoldDz, 32>::DZ < 25,
+              "folded tables reach the texture JBF's zero point (d = 25) with sat_fold_copies");
 
 // Frames one launch of the plain bilateral / adaptive kernels may filter (the
 // *_run_rows_batch entry points; a shard's B frames per RCCL group, vip_shard_run_batch).
@@ -411,7 +430,7 @@ struct LutStage {
 // [d][table][copy] layout, d = 0..DZ, at LDS byte T (the store() argument points there).
 template <int NT, class SL>
 struct SatStage {
-    static constexpr int WPD = SL::NTAB * 32;           // words per distance
+    static constexpr int WPD = SL::NTAB * SL::COPIES;   // words per distance
     static constexpr int N = (SL::DZ + 1) * WPD / 4;    // uint4 stores
     static constexpr int K = (N + NT - 1) / NT;
     uint32_t v[K];
@@ -420,7 +439,7 @@ struct SatStage {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int q = (int)threadIdx.x + k * NT;
-            const int w = 4 * q, d = w / WPD, t = (w - d * WPD) >> 5;
+            const int w = 4 * q, d = w / WPD, t = (w - d * WPD) / SL::COPIES;
             if (N % NT == 0 || q < N) v[k] = __float_as_uint(fold[t * kFoldEntries + d]);
         }
     }
