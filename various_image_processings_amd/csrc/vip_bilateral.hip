@@ -278,6 +278,13 @@ constexpr int max_waves() {
 #define VIP_BIL_SAT 0
 #endif
 
+// Joint kernel on the 512-entry saturating-address LUT (SatLut, 32 copies: no bank
+// conflicts) in place of the 16-copy 768-entry LUT, when the colour LUT is zero past 511
+// (sigma_color 30: past 432) and the tables leave as many waves (measurement knob).
+#ifndef VIP_JBF_SAT
+#define VIP_JBF_SAT 0
+#endif
+
 #ifndef VIP_JBF_SHORT_LUT  // joint kernel: 32-entry clamped LUT when the colour LUT allows it
 #define VIP_JBF_SHORT_LUT 0
 #endif
@@ -432,6 +439,13 @@ static int launch_bilateral_w(const StencilArgs& a, hipStream_t stream) {
     return (int)hipGetLastError();
 }
 
+template <int R>
+constexpr bool jbf_sat_fits() {
+    constexpr int P = outputs_per_thread<R, 2>();
+    return pick_waves_sat<R, 2, max_waves<R, 2>(), P, false>() >=
+           pick_waves<R, 2, max_waves<R, 2>(), 768 * lut_copies<R, 2>(), P>();
+}
+
 template <int R, bool JOINT, bool FMA>
 static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
     if constexpr (!JOINT && VIP_BIL_SAT) {  // plain filter, 128-pixel 16-wave tiles: 512 x 32 LUT (SatLut)
@@ -446,6 +460,8 @@ static int launch_bilateral_r(const StencilArgs& a, hipStream_t stream) {
             return launch_bilateral_ne<R, JOINT, FMA, 32, true, true>(a, stream);
     if constexpr (JOINT && VIP_JBF_SHORT_LUT)
         if (a.lut_nonzero <= 31) return launch_bilateral_ne<R, JOINT, FMA, 32>(a, stream);
+    if constexpr (JOINT && VIP_JBF_SAT && jbf_sat_fits<R>())
+        if (!a.fold && a.lut_nonzero <= 511) return launch_bilateral_ne<R, JOINT, FMA, 768, false, true>(a, stream);
     return launch_bilateral_ne<R, JOINT, FMA, 768>(a, stream);
 }
 
