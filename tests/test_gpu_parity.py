@@ -627,6 +627,28 @@ def test_kernel_timing_stamps_each_launch(dev, oracle):
         vip.kernel_timing(0).__enter__()
 
 
+def test_kernel_timing_leaves_captured_launches_plain(dev, oracle):
+    """A launch captured into a graph while the recorder is on takes no events (they would
+    never be stamped): the recorder counts nothing and the replayed graph filters exactly."""
+    from various_image_processings_amd.filters import _BilateralImpl
+    torch = dev.torch_
+    img = oracle.random_image(256, 128)
+    src, dst = dev.put(img), dev.empty((128, 256, 3))
+    b = _BilateralImpl(256, 128, 9)
+    s = torch.cuda.Stream()
+    b.bilateral_filter(src, dst, stream=s)  # first launch (LDS attribute) outside the capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with vip.kernel_timing(4) as kt:
+        with torch.cuda.graph(g, stream=s):
+            b.bilateral_filter(src, dst, stream=s)
+    assert kt.count == 0
+    dst.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(dev.get(dst), oracle.bilateral(img, 9))
+
+
 def test_small_frame_tiling_follows_frames_in_flight(dev, oracle):
     """The plain kernel's small-frame tiling counts the frames in flight (distinct streams
     among the device's last 8 launches): lenna-sized 512^2 frames on 4 streams take the

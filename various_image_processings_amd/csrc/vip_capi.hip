@@ -320,9 +320,14 @@ void note_launch(const void* kern) {
     if (g_nlaunched < 16) g_launched[g_nlaunched++] = kern;
 }
 
-LaunchEvents timing_events(const void* kern) {
+LaunchEvents timing_events(const void* kern, hipStream_t stream) {
     KernelTiming& t = g_timing;
     if (!t.on || t.n >= t.cap) return {nullptr, nullptr};
+    int dev = -1;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipGetDevice(&dev) != hipSuccess || dev != t.device || hipStreamIsCapturing(stream, &cap) != hipSuccess ||
+        cap != hipStreamCaptureStatusNone)
+        return {nullptr, nullptr};
     t.kern[t.n] = kern;
     const int i = t.n++;
     return {t.ev[2 * i], t.ev[2 * i + 1]};

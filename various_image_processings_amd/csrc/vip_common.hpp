@@ -95,11 +95,13 @@ inline int ensure_dynamic_lds(const void* kern, int bytes, std::atomic<unsigned 
 void note_launch(const void* kern);
 
 // Kernel-duration recorder of the calling thread (vip_kernel_timing_*, vip_capi.hip): while
-// it is on, the (start, stop) events for the next launch of `kern`, else two nulls.
+// it is on, the (start, stop) events for the next launch of `kern` on `stream`, else two
+// nulls (also for a launch on another device than the recorder's, or into a stream that is
+// being captured into a graph: its events would not be stamped).
 struct LaunchEvents {
     hipEvent_t start, stop;
 };
-LaunchEvents timing_events(const void* kern);
+LaunchEvents timing_events(const void* kern, hipStream_t stream);
 
 // Every stencil and texture launch goes through here: with the recorder on, the launch
 // carries an event pair that the runtime stamps with the kernel's own begin and end
@@ -107,7 +109,7 @@ LaunchEvents timing_events(const void* kern);
 // rocprofv3 --kernel-trace reports); otherwise a plain launch.
 template <typename K, typename... Args>
 inline void launch(K kern, dim3 grid, dim3 block, uint32_t lds, hipStream_t stream, Args... args) {
-    const LaunchEvents ev = timing_events(reinterpret_cast<const void*>(kern));
+    const LaunchEvents ev = timing_events(reinterpret_cast<const void*>(kern), stream);
     if (ev.start)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev.start, ev.stop, 0u, args...);
     else
