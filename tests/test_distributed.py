@@ -1,4 +1,4 @@
-"""Row-sharded multi-process path on CPU (gloo, world_size 2 and 3).
+"""Row-sharded multi-process path on CPU (gloo, world_size 2, 3 and 8).
 
 Each rank owns a row slab plus r-row halos; exchange_halo() fills the halos from
 the neighbouring ranks with point-to-point send/recv (the same calls run over
@@ -64,7 +64,9 @@ def _worker(rank, world, port, width, height, ksize, kind, nitr, out_dir):
 @pytest.mark.parametrize("world,height,ksize,kind,nitr", [(2, 37, 9, "bilateral", 0), (3, 50, 15, "bilateral", 0),
                                                           (2, 31, 31, "bilateral", 0),  # uneven 16/15-row shards, r=15
                                                           (2, 41, 7, "adaptive", 0), (2, 70, 5, "texture", 3),
-                                                          (3, 90, 3, "texture", 4)])
+                                                          (3, 90, 3, "texture", 4),
+                                                          (8, 83, 9, "bilateral", 0),  # the driver's N = 8, ragged
+                                                          (8, 371, 5, "texture", 5)])  # C4 k, nitr at N = 8: 46-row shards, 45-row halo
 def test_row_sharded_halo_exchange_matches_full_frame(tmp_path, world, height, ksize, kind, nitr):
     """Texture: one exchange of nitr * texture_halo_rows(k) rows per frame
     (ShardedTexture's ghost-zone scheme) makes each slab's own rows exact."""
