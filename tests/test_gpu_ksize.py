@@ -102,6 +102,18 @@ def test_texture_large_and_unit_ksize(dev, oracle, k, nitr, shape, numerics, pro
     assert np.array_equal(got, want), _mismatch(got, want)
 
 
+@pytest.mark.parametrize("k", [7, 9, 11, 13, 15])
+@pytest.mark.parametrize("numerics,profile", PROFILES)
+def test_texture_guide_tiles_across_tile_seams(dev, oracle, k, numerics, profile):
+    """Texture ksize 7-15, the per-radius guide-stage tiles (vip_texture.hip GfTile: 92 x 32
+    at R = 3-5, 64 x 16 at R = 6, 60 x 36 with capped VGPRs at R = 7), on a frame several
+    tiles wide and tall with partial tiles on the right and bottom edges."""
+    img = _img(oracle, 157, 263, seed_rev=True)
+    got = _run_texture(dev, img, k, 2, numerics)
+    want = oracle.texture(img, k, 2, profile)
+    assert np.array_equal(got, want), _mismatch(got, want)
+
+
 # One full-width 3840-pixel band per filter at its largest ksize: a 3840 x 200 frame
 # (rows 0..199 with the replicate border on top), checked on rows crossing the top
 # border and an interior tile seam.
