@@ -9,7 +9,8 @@ drawn over decades), the numerics profile, the input statistics (uniform, narrow
 ABI's pitch argument -- row padding. 48 cases, each small enough for the oracle to finish
 in well under a second; a second sweep drives the multi-frame launches (run_rows_batch: row
 bands of 2-6 frames, free CUs, frames in flight, and so the cut last round). VIP_FUZZ_CASES /
-VIP_FUZZ_BATCH_CASES widen the sweeps for a one-off run (profiles/r05_fuzz_wide.log).
+VIP_FUZZ_BATCH_CASES widen the sweeps for a one-off run (profiles/r05_fuzz_wide.log), and
+VIP_FUZZ_SEED draws other cases.
 """
 import os
 
@@ -23,10 +24,11 @@ pytestmark = pytest.mark.gpu
 
 N_CASES = int(os.environ.get("VIP_FUZZ_CASES", 48))
 N_BATCH_CASES = int(os.environ.get("VIP_FUZZ_BATCH_CASES", 24))
+SEED0 = int(os.environ.get("VIP_FUZZ_SEED", 0))  # another draw of cases for a one-off run
 
 
 def _case(i):
-    r = np.random.default_rng(1000 + i)
+    r = np.random.default_rng(SEED0 + 1000 + i)
     kind = ["bilateral", "joint", "adaptive", "texture"][i % 4]
     h, w = int(r.integers(1, 160)), int(r.integers(1, 300))
     if kind == "texture":
@@ -42,7 +44,8 @@ def _case(i):
     data = ["uniform", "narrow", "ramp"][int(r.integers(0, 3))]
     # extra bytes per row (the C ABI's pitch; vip_texture_run takes dense frames)
     pad = 0 if kind == "texture" else int(r.choice([0, 0, 1, 13, 64]))
-    return dict(kind=kind, h=h, w=w, k=k, nitr=nitr, ss=ss, sc=sc, profile=profile, data=data, pad=pad, seed=1000 + i)
+    return dict(kind=kind, h=h, w=w, k=k, nitr=nitr, ss=ss, sc=sc, profile=profile, data=data, pad=pad,
+                seed=SEED0 + 1000 + i)
 
 
 def _image(c, salt=0):
@@ -113,7 +116,7 @@ def test_random_case_bit_exact(dev, oracle, i):
 
 
 def _batch_case(i):
-    r = np.random.default_rng(5000 + i)
+    r = np.random.default_rng(SEED0 + 5000 + i)
     kind = ["bilateral", "adaptive"][i % 2]
     k = int(r.choice([1, 3, 5, 7, 9, 11, 13, 15, 17]))  # the multi-frame kernels' radii (<= 8)
     h, w = int(r.integers(1, 200)), int(r.integers(1, 700))
@@ -122,7 +125,7 @@ def _batch_case(i):
     return dict(kind=kind, k=k, h=h, w=w, row0=row0, out_rows=out_rows, n=int(r.integers(2, 7)),
                 free=int(r.choice([0, 0, 8, 16, 64, int(r.integers(0, 256))])), inflight=int(r.integers(0, 3)),
                 ss=float(10 ** r.uniform(-0.5, 2.5)), sc=float(10 ** r.uniform(-0.3, 2.3)),
-                profile=int(r.integers(0, 2)), seed=5000 + i)
+                profile=int(r.integers(0, 2)), seed=SEED0 + 5000 + i)
 
 
 @pytest.mark.parametrize("i", range(N_BATCH_CASES))
